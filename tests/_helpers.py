@@ -1,0 +1,78 @@
+"""Shared parity helpers for the test-suite (golden-fixture loading, tie-aware top-k check)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# Score tolerance written in the north star: fp32 scores within 1e-4 of the reference.
+SCORE_ATOL = 1e-4
+
+
+def load_golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def params_from(z, tag):
+    pre = tag + "/"
+    return {k[len(pre):]: z[k] for k in z.files if k.startswith(pre) and k.count("/") == 1
+            and ("." in k[len(pre):])}
+
+
+def positives_from(z, kind):
+    flat, lens = z[kind + "_flat"], z[kind + "_len"]
+    out, o = [], 0
+    for n in lens:
+        out.append([int(x) for x in flat[o:o + n]])
+        o += n
+    return out
+
+
+def tie_groups(scores, tie_eps):
+    """Split a descending score list into maximal runs whose neighbours differ by <= tie_eps."""
+    groups, start = [], 0
+    for i in range(1, len(scores) + 1):
+        if i == len(scores) or (scores[i - 1] - scores[i]) > tie_eps or np.isnan(scores[i]) != np.isnan(scores[i - 1]):
+            groups.append((start, i))
+            start = i
+    return groups
+
+
+def assert_topk_equivalent(ref_ids, ref_scores, our_ids, our_scores, tie_eps,
+                           score_atol=SCORE_ATOL, lookup=None):
+    """Tie-aware top-k parity (SURVEY.md 8(a) 'Tie rule').
+
+    Wherever the reference's sorted scores are separated by more than `tie_eps`, the id at
+    each position must be identical. Inside a run of scores within `tie_eps` of each other the
+    ids are compared as a set; for the run that straddles rank k, each of our ids that the
+    reference did not list must carry a score within `tie_eps` of that run (its reference score
+    when `lookup` (id -> reference score) is given, else our own). Scores at equal positions
+    must agree within `score_atol`.
+    """
+    ref_ids = [int(x) for x in ref_ids]
+    our_ids = [int(x) for x in our_ids]
+    ref_scores = np.asarray(ref_scores, dtype=np.float64)
+    our_scores = np.asarray(our_scores, dtype=np.float64)
+    k = len(ref_ids)
+    assert len(our_ids) == k, (len(our_ids), k)
+    assert len(set(our_ids)) == k, "duplicate ids in top-k"
+    both = ~(np.isnan(ref_scores) | np.isnan(our_scores))
+    assert np.array_equal(np.isnan(ref_scores), np.isnan(our_scores))
+    assert np.all(np.abs(ref_scores[both] - our_scores[both]) <= score_atol), \
+        np.max(np.abs(ref_scores[both] - our_scores[both]))
+    groups = tie_groups(ref_scores, tie_eps)
+    for gi, (a, b) in enumerate(groups):
+        r, o = set(ref_ids[a:b]), set(our_ids[a:b])
+        if gi < len(groups) - 1:
+            assert r == o, f"positions {a}:{b}: ref {sorted(r)} ours {sorted(o)}"
+        else:
+            lo = ref_scores[b - 1] - tie_eps
+            hi = ref_scores[a] + tie_eps
+            for pos in range(a, b):
+                c = our_ids[pos]
+                if c in r:
+                    continue
+                s = lookup[c] if lookup is not None and c in lookup else our_scores[pos]
+                assert lo <= s <= hi, f"id {c} at pos {pos} score {s} outside tie run [{lo},{hi}]"

@@ -1,0 +1,107 @@
+"""Pin the CPU oracle against golden vectors captured from the reference (tests/golden/).
+
+CPU-only. These tests are what make the oracle trustworthy as the GPU parity checker.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from _helpers import (assert_topk_equivalent, load_golden, params_from, positives_from)
+from oracle import metrics_oracle, nais_oracle, powerlaw_oracle
+
+# fp32 CPU restatement vs the reference's torch CPU kernels: different GEMM summation orders
+# differ by a few ulps; 1e-6 on sigmoid scores is ~16 ulp at 0.5.
+ORACLE_ATOL = 1e-6
+ORACLE_TIE_EPS = 2e-7
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 5, 20])
+def test_forward_basic(tag, n):
+    z = load_golden("forward_basic.npz")
+    p = params_from(z, tag)
+    hist, tgt, ref = z[f"{tag}/n{n}/hist"], z[f"{tag}/n{n}/target"], z[f"{tag}/n{n}/pred"]
+    got, nan_count = nais_oracle.forward_basic(p, hist, tgt)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert nan_count == int(np.isnan(ref).sum())
+    if n == 1:
+        assert nan_count == 8          # rows 0..7: single-item history == target -> 0/0
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+
+
+@pytest.mark.parametrize("variant", ["region", "region_distance"])
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 7])
+def test_forward_region(variant, tag, n):
+    z = load_golden(f"forward_{variant}.npz")
+    p = params_from(z, tag)
+    region_of = z[f"{tag}/region_of"]
+    hist, tgt, ref = z[f"{tag}/n{n}/hist"], z[f"{tag}/n{n}/target"], z[f"{tag}/n{n}/pred"]
+    if variant == "region":
+        logit = nais_oracle.attention_region(p, hist, tgt, region_of[hist], region_of[tgt])
+    else:
+        ll = nais_oracle.latlon_pairs(z["coords"], np.broadcast_to(tgt[:, None], hist.shape), hist)
+        logit = nais_oracle.attention_region_distance(p, hist, tgt, region_of[hist],
+                                                      region_of[tgt], ll.astype(np.float32))
+    got = nais_oracle._sigmoid(logit)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+
+
+def _catalog(variant, z, p, u):
+    P = int(z["num_pois"])
+    hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
+    if variant == "basic":
+        return nais_oracle.catalog_scores_basic(p, hist, P)
+    if variant == "region":
+        return nais_oracle.catalog_scores_region(p, hist, P, z["region_of"])
+    return nais_oracle.catalog_scores_region_distance(p, hist, P, z["region_of"], z["coords"])
+
+
+@pytest.mark.parametrize("variant", ["basic", "region", "region_distance"])
+@pytest.mark.parametrize("tag", ["init", "trained"])
+def test_catalog_topk(variant, tag):
+    z = load_golden(f"catalog_{variant}.npz")
+    p = params_from(z, tag)
+    U = int(z["num_users"])
+    recs = []
+    for u in range(U):
+        cand, sc = _catalog(variant, z, p, u)
+        key = f"{tag}/full_scores_u{u}"
+        if key in z.files:
+            np.testing.assert_allclose(sc, z[key], rtol=0, atol=ORACLE_ATOL)
+        ids, top = nais_oracle.topk_ids(cand, sc, 50)
+        lookup = dict(zip(cand.tolist(), sc.tolist()))
+        assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids, top,
+                               tie_eps=ORACLE_TIE_EPS, lookup=lookup)
+        recs.append(ids.tolist())
+    # metrics restatement reproduces the reference's 6-tuple on the reference's own lists
+    ref_lists = [list(map(int, r)) for r in z[f"{tag}/topk_ids"]]
+    k_list = [5, 10, 15, 20, 25, 30]
+    val = metrics_oracle.evaluate(positives_from(z, "val"), ref_lists, k_list)
+    test = metrics_oracle.evaluate(positives_from(z, "test"), ref_lists, k_list)
+    np.testing.assert_array_equal(np.array(val + test), z[f"{tag}/metrics"])
+
+
+def test_powerlaw_dist_prd_predict():
+    z = load_golden("powerlaw.npz")
+    d = [powerlaw_oracle.dist(tuple(a), tuple(b)) for a, b in zip(z["dist_a"], z["dist_b"])]
+    np.testing.assert_array_equal(np.array(d), z["dist"])
+    assert np.all(z["dist"][:80] == 0.0)
+    a, b = z["pr_d_ab"]
+    np.testing.assert_array_equal(np.array([powerlaw_oracle.pr_d(a, b, x) for x in z["pr_d_in"]]),
+                                  z["pr_d"])
+    ip, ix, co = z["pl_indptr"], z["pl_indices"], z["pl_coords"]
+    fa, fb = powerlaw_oracle.fit(ip, ix, co, *z["fit_w_init"])
+    assert (fa, fb) == tuple(z["fit_ab"])
+    pred = np.array([[powerlaw_oracle.predict(fa, fb, co, ix[ip[u]:ip[u + 1]], int(c))
+                      for c in z["predict_cands"]] for u in range(len(ip) - 1)])
+    np.testing.assert_array_equal(pred, z["predict"])
+    assert np.all(z["predict"][-1] == 0.0) or np.any(z["predict"][-1] < 1e-300)
+    norm = np.array([powerlaw_oracle.normalize(list(r)) for r in z["normalize_in"]])
+    np.testing.assert_array_equal(norm, z["normalize"])
+    assert powerlaw_oracle.normalize([0.0, 0.0, 0.0]) == list(z["normalize_zero"])
+    assert not any(math.isnan(x) for x in d)
