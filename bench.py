@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: full-catalog NAIS scoring + top-50, scored (user, POI) pairs/s (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3], the "100k POIs" metric config): synthetic Gowalla-scale
+check-ins, 50k users x 100k POIs, d = H = 64, h_u ~ U{1..200}, k = 50, NAIS_basic, fp32.
+A step = one batch of `--users-per-step` users per GPU: every catalog POI is scored against the
+user's whole history by the fused HIP kernel (nais_score_catalog), then a per-user radix-select
+top-50 (nais_topk_rows), then (N > 1) the per-step top-k lists are all-gathered over RCCL.
+Inputs (tables, CSR, user lists) are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torchrun); users are sharded across ranks by LPT on the cost
+(P - h_u) * h_u, the POI tables are replicated by an RCCL broadcast from rank 0.
+Per-GPU work per step is fixed -> weak scaling.
+"""
+from __future__ import annotations
+
+import argparse
+import heapq
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense), spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--users-per-step", type=int, default=256)
+    ap.add_argument("--num-users", type=int, default=50_000)
+    ap.add_argument("--num-pois", type=int, default=100_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--hidden", type=int, default=64)
+    ap.add_argument("--h-max", type=int, default=200)
+    ap.add_argument("--topk", type=int, default=50)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def shard_users(hist_len, P, world):
+    """LPT: heaviest user to the least-loaded rank (SURVEY.md 8(e) partitioning)."""
+    cost = (P - hist_len) * hist_len
+    order = np.argsort(-cost, kind="stable")
+    heap = [(0, r) for r in range(world)]
+    out = [[] for _ in range(world)]
+    for u in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(int(u))
+        heapq.heappush(heap, (load + int(cost[u]), r))
+    return [np.array(x, dtype=np.int64) for x in out]
+
+
+def cpu_baseline(p, data, users, k, seconds):
+    """The CPU restatement (oracle, numpy fp32 + BLAS threads) on a bounded user sample."""
+    from oracle import nais_oracle
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count()
+    pairs, t0, n = 0, time.perf_counter(), 0
+    for u in users:
+        cand, sc = nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois)
+        nais_oracle.topk_ids(cand, sc, k)
+        pairs += len(cand)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": int(cores), "kind": "port",
+            "sample": f"{n} users of the same workload (complement candidates + chunked forward + "
+                      f"top-{k}, oracle/nais_oracle.py numpy fp32), {pairs} pairs in {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from poi_recommendation_models_amd import _capi
+    from poi_recommendation_models_amd.catalog import DeviceCSR
+    from poi_recommendation_models_amd.model import NAIS_basic
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+
+    P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
+    data = make_checkins(a.num_users, P, a.h_max, seed=2024)
+    model = NAIS_basic(P, D, H, 0.5)
+    p_host = None
+    if rank == 0:
+        p_host = init_nais_params(P, D, H, seed=7, emb_std=0.3, bias_std=0.1)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in p_host.items()}, strict=False)
+    model = model.to(dev).eval()
+    model.report_nan = False
+    if world > 1:   # replicate the POI tables + MLP over RCCL (xGMI), once
+        for t in model.state_dict().values():
+            dist.broadcast(t, src=0)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
+    hist_len = data.hist_len()
+    mine = shard_users(hist_len, P, world)[rank]
+    rng = np.random.default_rng(100 + rank)
+    rng.shuffle(mine)                      # every step is a representative sample of h_u
+    B = a.users_per_step
+    nsteps = a.warmup + a.steps
+    steps = []
+    for s in range(nsteps):
+        us = np.take(mine, np.arange(s * B, (s + 1) * B), mode="wrap")
+        c = (P - hist_len[us]) * hist_len[us]
+        us = us[np.argsort(-c, kind="stable")]          # heavy users dispatched first
+        steps.append((torch.from_numpy(us.astype(np.int32)).to(dev),
+                      int((P - hist_len[us]).sum()),
+                      int(((P - hist_len[us]) * hist_len[us]).sum())))
+    lib = _capi.load()
+    prm = model.nais_params()
+    scores = torch.empty(B, P, dtype=torch.float32, device=dev)
+    ids = torch.empty(B, K, dtype=torch.int32, device=dev)
+    top = torch.empty(B, K, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    gat_ids = torch.empty(world * B, K, dtype=torch.int32, device=dev) if world > 1 else None
+    gat_sc = torch.empty(world * B, K, dtype=torch.float32, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(s, ev=None):
+        u_dev = steps[s][0]
+        if ev is not None:
+            ev[0].record(stream)
+        _capi.check(lib.nais_score_catalog(prm, csr.indptr.data_ptr(), csr.indices.data_ptr(),
+                                           u_dev.data_ptr(), B, None, None, None, scores.data_ptr(),
+                                           P, cnt[0:1].data_ptr(), sh), "score_catalog")
+        if ev is not None:
+            ev[1].record(stream)
+        _capi.check(lib.nais_topk_rows(scores.data_ptr(), P, P, B, K, ids.data_ptr(), top.data_ptr(),
+                                       cnt[1:2].data_ptr(), sh), "topk_rows")
+        if ev is not None:
+            ev[2].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gat_ids, ids)
+            dist.all_gather_into_tensor(gat_sc, top)
+
+    for s in range(a.warmup):
+        step(s)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i, evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    pairs = sum(steps[a.warmup + i][1] for i in range(a.steps))
+    work = sum(steps[a.warmup + i][2] for i in range(a.steps))
+    score_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(a.steps)]
+    topk_ms = [evs[i][1].elapsed_time(evs[i][2]) for i in range(a.steps)]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        pt = torch.tensor([pairs], dtype=torch.float64, device=dev)
+        dist.all_reduce(pt)
+        pairs_total = float(pt.item())
+    else:
+        pairs_total = float(pairs)
+
+    flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
+    flops = work * flop_per_pair_item / a.steps          # algorithmic FLOP per catalog launch
+    avg_score_s = float(np.mean(score_ms)) / 1e3
+    achieved = flops / avg_score_s / 1e12
+    traffic = None
+    try:
+        tj = json.load(open(a.traffic_json))
+        if tj.get("users_per_launch") == B and tj.get("num_pois") == P and tj.get("dim") == D:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(p_host, data, mine[:64], K, a.cpu_seconds)
+        out = {
+            "metric": "scored (user,POI) pairs/sec full-catalog + top-50, 100k POIs",
+            "value": pairs_total / elapsed,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
+            "config": {
+                "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
+                            "score + top-%d" % (a.num_users, P, D, K),
+                "model": "NAIS_basic", "users_per_step_per_gpu": B, "num_pois": P,
+                "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,
+                "pairs_per_step_per_gpu": pairs / a.steps,
+                "parallelism": f"users sharded (LPT) over {world} GPU(s), POI tables replicated",
+            },
+            "roofline": {
+                "kernel": "catalog_score_kernel (nais_score_catalog)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": PEAK_FP32_MFMA_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+                "traffic": traffic,
+                "algorithmic_flop_per_launch": flops,
+                "avg_launch_ms": avg_score_s * 1e3,
+                "topk_avg_launch_ms": float(np.mean(topk_ms)),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

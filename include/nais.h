@@ -1,0 +1,165 @@
+/*
+ * nais.h -- C-ABI of the MI355X-native NAIS scoring path (gfx950, libnais_hip.so).
+ *
+ * The reference (muyeon-jo/POI_recommendation_models) is pure Python + PyTorch and exposes no
+ * FFI; the boundary this library replaces is the Python call surface of its NAIS hot path:
+ *
+ *   nais_forward        replaces NAIS_basic.forward            model.py:40-55  (+ attention_network :57-89)
+ *                                NAIS_regionEmbedding.forward   model.py:132-142 (+ :144-180)
+ *                                NAIS_region_distance_Embedding.forward model.py:231-244 (+ :246-297)
+ *   nais_score_topk     replaces the per-user loop body of      validation.py:11-27 (NAIS_validation),
+ *                                                               validation.py:38-55 (NAIS_region_validation),
+ *                                                               validation.py:69-127 (NAIS_region_distance_validation)
+ *                       i.e. get_NAIS_batch_test* (batches.py:52-65, 110-139) + chunked forward + torch.topk
+ *   nais_gather_rows    the embedding gather of model.py:64 (nn.Embedding -> index_select) as a standalone
+ *                       HBM-roofline kernel
+ *
+ * Conventions: every pointer is caller-owned DEVICE memory (e.g. torch tensor.data_ptr()); the library
+ * never allocates, frees or copies caller memory, never synchronises, and issues all work on `stream`
+ * (a hipStream_t; NULL = legacy default stream). Calls are asynchronous and stream-ordered.
+ * Scratch memory comes from a caller-supplied workspace sized by the matching *_workspace_size().
+ * Return value: 0 on success, < 0 on error (see NAIS_E_*); nais_last_error() then describes it
+ * (thread-local). All arithmetic is IEEE fp32 (fp64 for coordinates), as in the reference.
+ */
+#ifndef NAIS_H_
+#define NAIS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NAIS_ABI_VERSION 1
+
+/* model variants */
+#define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
+#define NAIS_VARIANT_REGION 1          /* NAIS_regionEmbedding            model.py:99-187  */
+#define NAIS_VARIANT_REGION_DISTANCE 2 /* NAIS_region_distance_Embedding  model.py:189-304 */
+
+/* flags for nais_forward */
+#define NAIS_FLAG_SIGMOID 1            /* apply sigmoid (model.py:55); else return the logits of attention_network */
+
+/* error codes */
+#define NAIS_OK 0
+#define NAIS_E_INVALID (-1)            /* bad pointer / shape / dtype-implied size */
+#define NAIS_E_UNSUPPORTED (-2)        /* a dimension outside the compiled kernel set */
+#define NAIS_E_HIP (-3)                /* a HIP runtime error while launching */
+#define NAIS_E_WORKSPACE (-4)          /* workspace missing or too small */
+
+/*
+ * Parameters of one NAIS model: device pointers to the reference's nn.Module parameters
+ * (state_dict names in comments) plus their dimensions. embed_dim must be a multiple of 8.
+ */
+typedef struct nais_params {
+  int32_t variant;              /* NAIS_VARIANT_* */
+  int32_t embed_dim;            /* D: width of h_j (.) t. basic: embed_size; region*: embed_size      */
+  int32_t item_dim;             /* columns of embed_history/embed_target: D (basic) or D/2 (region*)  */
+  int32_t region_dim;           /* columns of embed_region: D/2 (region*), 0 (basic)                   */
+  int32_t hidden;               /* H = attn_layer1.out_features (1..128)                               */
+  int32_t din;                  /* attn_layer1.in_features: D, or D+2 for region_distance              */
+  int64_t num_pois;             /* P = rows of embed_history / embed_target                            */
+  int64_t num_regions;          /* R = rows of embed_region (0 for basic)                              */
+  float beta;                   /* attention smoothing exponent (model.py:80), 0.5 in every driver     */
+  float _pad0;
+  const float* embed_history;   /* embed_history.weight [P, item_dim]        model.py:15,106,198      */
+  const float* embed_target;    /* embed_target.weight  [P, item_dim]        model.py:16,107,199      */
+  const float* embed_region;    /* embed_region.weight  [R, region_dim]|NULL model.py:109,203         */
+  const float* w1;              /* attn_layer1.weight   [H, din]             model.py:25,116,212      */
+  const float* b1;              /* attn_layer1.bias     [H]                                           */
+  const float* w2;              /* attn_layer2.weight   [1, H]               model.py:26,117,213      */
+  const float* dist_w;          /* dist_layer.weight    [2, 2] | NULL        model.py:215             */
+  const float* dist_b;          /* dist_layer.bias      [2]    | NULL                                 */
+} nais_params_t;
+
+/* Optional power-law geo prior blended into the catalog scores (powerLaw.py:86-92, run.py:55-59,
+ * run.py:537-539): score' = (1-alpha)*score + alpha * G(u,c)/max_c G(u,c), G = prod_j a*max(0.01,dist)^b.
+ * Not yet implemented in ABI v1: pass NULL. */
+typedef struct nais_prior {
+  double a, b, alpha;
+  const double* coords;         /* [P, 2] (lat, lng) float64 */
+} nais_prior_t;
+
+/* ABI version of the loaded library (== NAIS_ABI_VERSION it was built with). */
+int32_t nais_abi_version(void);
+
+/* Thread-local description of the last error returned by this thread. */
+const char* nais_last_error(void);
+
+/*
+ * General forward (any per-row histories): for row r in [0,b) with history hist[r*hist_ld + j],
+ * j in [0,n), and target item target[r], write out[r] = sigmoid(logit) (flags & NAIS_FLAG_SIGMOID)
+ * or the logit of attention_network, exactly as model.py:57-89 (mask model.py:92-95, no
+ * max-subtraction, beta-smoothed denominator). n == 0 gives logit 0.
+ *   hist_region [b, n] (row stride hist_region_ld), target_region [b]: region variants only.
+ *   target_lat_long [b, n, 2] f32 (row stride latlon_ld, in elements): region_distance only,
+ *   = (|lat_c - lat_j|, |lng_c - lng_j|) as built at run.py:47-54 / validation.py:108-118.
+ *   nan_count (may be NULL): device int32, atomically incremented by the number of NaN logits
+ *   (model.py:50-54 prints this count).
+ */
+int32_t nais_forward(const nais_params_t* params,
+                     const int64_t* hist, int64_t b, int64_t n, int64_t hist_ld,
+                     const int64_t* target,
+                     const int64_t* hist_region, int64_t hist_region_ld,
+                     const int64_t* target_region,
+                     const float* target_lat_long, int64_t latlon_ld,
+                     float* out, int32_t* nan_count, int32_t flags, void* stream);
+
+/*
+ * Full-catalog scoring + top-k for a list of users (validation.py:11-27 per-user body):
+ * candidates of user u are every POI not in its training history
+ *   indices[indptr[u] .. indptr[u+1])   (CSR of train_matrix, batches.py:55-56),
+ * each scored with the variant's forward (sigmoid), then the k best are returned ordered by
+ * (score desc, POI id asc); NaN ranks first (torch.topk semantics).
+ *   users[i] (i < num_users): user ids to score; out_ids / out_scores are [num_users, k].
+ *   region_of [P] int64: POI -> region (businessRegionEmbedList, run.py:149-152), region variants.
+ *   coords [P, 2] float64 (lat, lng): region_distance -- (|dlat|, |dlng|) formed on the fly in
+ *   float64, bit-identical to run.py:47-54. latlon_mat [P, P, 2] float64: the reference's own
+ *   matrix (run.py:214), read instead when coords is NULL (feasible only for small P).
+ *   k <= 1024 and every user needs at least k candidates (torch.topk raises otherwise; the
+ *   caller checks -- the kernel writes id -1 / NaN for missing slots and counts them in *short_count).
+ *   nan_count / short_count (device int32, may be NULL) are atomically incremented.
+ */
+size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k);
+int32_t nais_score_topk(const nais_params_t* params,
+                        const int64_t* indptr, const int64_t* indices,
+                        const int32_t* users, int32_t num_users, int32_t k,
+                        const int64_t* region_of, const double* coords,
+                        const double* latlon_mat, const nais_prior_t* prior,
+                        int32_t* out_ids, float* out_scores,
+                        int32_t* nan_count, int32_t* short_count,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Scores only (the first half of nais_score_topk): scores[i * score_ld + c] = sigmoid score of POI c
+ * for user users[i], c in [0, P); POIs in the user's history are written as -1.0f (they are not
+ * candidates, batches.py:56). score_ld >= P. Used for parity tests and by callers that post-process
+ * the full score row (e.g. the geo-prior blend).
+ */
+int32_t nais_score_catalog(const nais_params_t* params,
+                           const int64_t* indptr, const int64_t* indices,
+                           const int32_t* users, int32_t num_users,
+                           const int64_t* region_of, const double* coords, const double* latlon_mat,
+                           float* scores, int64_t score_ld, int32_t* nan_count, void* stream);
+
+/*
+ * Top-k of score rows (the second half of nais_score_topk): for row i in [0, num_rows), the k largest
+ * entries of scores[i * score_ld + c], c in [0, P), ignoring negative entries (non-candidates), ordered
+ * (score desc, c asc), NaN first -> out_ids / out_scores [num_rows, k]. k <= 1024.
+ */
+int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, int32_t num_rows,
+                       int32_t k, int32_t* out_ids, float* out_scores, int32_t* short_count,
+                       void* stream);
+
+/*
+ * Standalone embedding-row gather (model.py:64, nn.Embedding): out[i, :] = table[idx[i], :],
+ * table [rows, dim] f32 row-major, idx [m] int64 (caller guarantees 0 <= idx < rows).
+ */
+int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
+                         const int64_t* idx, int64_t m, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NAIS_H_ */

@@ -1,0 +1,97 @@
+"""ctypes binding of the C-ABI in include/nais.h (libnais_hip.so, built for gfx950).
+
+There is deliberately no fallback: if the shared library is missing or fails to load, every
+product entry point raises. The CPU restatement under oracle/ is test infrastructure only.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libnais_hip.so"
+LIB_PATH = os.path.join(HERE, LIB_NAME)
+
+ABI_VERSION = 1
+VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE = 0, 1, 2
+FLAG_SIGMOID = 1
+
+EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_topk_workspace_size",
+           "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_gather_rows")
+
+
+class NaisParams(ctypes.Structure):
+    """Mirror of `nais_params_t` (include/nais.h)."""
+    _fields_ = [
+        ("variant", ctypes.c_int32), ("embed_dim", ctypes.c_int32), ("item_dim", ctypes.c_int32),
+        ("region_dim", ctypes.c_int32), ("hidden", ctypes.c_int32), ("din", ctypes.c_int32),
+        ("num_pois", ctypes.c_int64), ("num_regions", ctypes.c_int64),
+        ("beta", ctypes.c_float), ("_pad0", ctypes.c_float),
+        ("embed_history", ctypes.c_void_p), ("embed_target", ctypes.c_void_p),
+        ("embed_region", ctypes.c_void_p), ("w1", ctypes.c_void_p), ("b1", ctypes.c_void_p),
+        ("w2", ctypes.c_void_p), ("dist_w", ctypes.c_void_p), ("dist_b", ctypes.c_void_p),
+    ]
+
+
+class NaisError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load (once) and type the shared library; raises NaisError if it cannot be loaded."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("NAIS_HIP_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise NaisError(f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                        "(hipcc --offload-arch=gfx950); there is no CPU fallback for the NAIS path")
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError as e:
+        raise NaisError(f"failed to load {p}: {e}") from e
+    vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+    lib.nais_abi_version.restype = i32
+    lib.nais_abi_version.argtypes = []
+    lib.nais_last_error.restype = ctypes.c_char_p
+    lib.nais_last_error.argtypes = []
+    lib.nais_forward.restype = i32
+    lib.nais_forward.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, i64, vp, vp,
+                                 i64, vp, vp, i32, vp]
+    lib.nais_score_topk_workspace_size.restype = sz
+    lib.nais_score_topk_workspace_size.argtypes = [ctypes.POINTER(NaisParams), i32, i32]
+    lib.nais_score_topk.restype = i32
+    lib.nais_score_topk.argtypes = [ctypes.POINTER(NaisParams), vp, vp, vp, i32, i32, vp, vp, vp,
+                                    vp, vp, vp, vp, vp, vp, sz, vp]
+    lib.nais_score_catalog.restype = i32
+    lib.nais_score_catalog.argtypes = [ctypes.POINTER(NaisParams), vp, vp, vp, i32, vp, vp, vp, vp,
+                                       i64, vp, vp]
+    lib.nais_topk_rows.restype = i32
+    lib.nais_topk_rows.argtypes = [vp, i64, i64, i32, i32, vp, vp, vp, vp]
+    lib.nais_gather_rows.restype = i32
+    lib.nais_gather_rows.argtypes = [vp, i64, i32, vp, i64, vp, vp]
+    v = lib.nais_abi_version()
+    if v != ABI_VERSION:
+        raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().nais_last_error().decode(errors="replace")
+        raise NaisError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,37 @@
+"""Build libnais_hip.so in-tree for gfx950 (hipcc; no torch extension machinery needed)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "nais_kernels.hip")
+OUT = os.path.join(HERE, "libnais_hip.so")
+ARCH = os.environ.get("NAIS_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build(force=False, extra=()):
+    deps = [SRC, os.path.join(ROOT, "include", "nais.h")]
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+        return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC, *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed ({r.returncode}): {' '.join(cmd)}")
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,149 @@
+"""Full-catalog scoring + top-k on the device (the per-user body of validation.py:11-27).
+
+`score_topk` replaces, for a whole set of users at once:
+  get_NAIS_batch_test(train_matrix, u)   batches.py:52-65   (complement candidates, C_u x h int64 matrix, H2D)
+  chunked model(user_history, target)    validation.py:14-22 (1,024-row forward chunks, NaN .item() per chunk)
+  torch.topk(pred, k) + 50 .item()       validation.py:26-27
+with one `nais_score_topk` call: the user's CSR row is read on the device, every POI of the
+catalog is scored by the fused kernel (history POIs excluded), and a radix-select top-k runs
+per user. Nothing per-candidate crosses PCIe.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _capi
+
+
+class DeviceCSR:
+    """train_matrix (scipy CSR, users x POIs) resident on the device as int64 indptr/indices."""
+
+    def __init__(self, train_matrix, device):
+        X = train_matrix.tocsr() if not hasattr(train_matrix, "indptr") else train_matrix
+        self.shape = X.shape
+        self.host_indptr = np.asarray(X.indptr, dtype=np.int64)
+        self.host_indices = np.asarray(X.indices, dtype=np.int64)
+        self.hist_len = np.diff(self.host_indptr)
+        self.indptr = torch.from_numpy(self.host_indptr).to(device)
+        self.indices = torch.from_numpy(self.host_indices).to(device)
+        self.device = device
+        self.key = (id(train_matrix), X.shape, X.nnz)
+
+    @classmethod
+    def from_arrays(cls, indptr, indices, num_pois, device):
+        import scipy.sparse as sp
+        X = sp.csr_matrix((np.ones(len(indices)), np.asarray(indices), np.asarray(indptr)),
+                          shape=(len(indptr) - 1, num_pois))
+        return cls(X, device)
+
+
+_csr_cache: dict = {}
+_ws_cache: dict = {}
+
+
+def device_csr(train_matrix, device) -> DeviceCSR:
+    if isinstance(train_matrix, DeviceCSR):
+        return train_matrix
+    X = train_matrix
+    key = (id(X), X.shape, X.nnz, str(device))
+    hit = _csr_cache.get(key)
+    if hit is None or hit[0] is not X:
+        _csr_cache.clear()
+        hit = (X, DeviceCSR(X, device))
+        _csr_cache[key] = hit
+    return hit[1]
+
+
+def _workspace(device, nbytes):
+    ws = _ws_cache.get(str(device))
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _ws_cache[str(device)] = ws
+    return ws
+
+
+def lpt_order(users, hist_len, num_pois):
+    """Users sorted by descending cost (P - h_u) * h_u: heaviest workgroups are dispatched first."""
+    users = np.asarray(users, dtype=np.int64)
+    h = hist_len[users]
+    cost = (num_pois - h) * h
+    return users[np.argsort(-cost, kind="stable")]
+
+
+def _side_inputs(model, dev, region_of, coords, latlon_mat):
+    reg = cor = llm = None
+    if model.VARIANT != _capi.VARIANT_BASIC:
+        if region_of is None:
+            raise ValueError("region variants need businessRegionEmbedList (POI -> region)")
+        reg = torch.as_tensor(np.asarray(region_of, dtype=np.int64)).to(dev)
+    if model.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+        if coords is not None:
+            cor = torch.as_tensor(np.ascontiguousarray(coords, dtype=np.float64)).to(dev)
+        elif latlon_mat is not None:
+            llm = torch.as_tensor(np.ascontiguousarray(latlon_mat, dtype=np.float64)).to(dev)
+        else:
+            raise ValueError("region_distance needs poi coords (or the reference latlon_mat)")
+    return reg, cor, llm
+
+
+def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlon_mat=None):
+    """Full score rows f32 [len(users), P] (history POIs = -1.0), via nais_score_catalog."""
+    dev = model._check_device()
+    csr = device_csr(train_matrix, dev)
+    P = model.embed_history.weight.shape[0]
+    users = np.asarray(list(users), dtype=np.int64)
+    u_dev = torch.from_numpy(users.astype(np.int32)).to(dev)
+    reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
+    out = torch.empty(len(users), P, dtype=torch.float32, device=dev)
+    nan = torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = _capi.load().nais_score_catalog(model.nais_params(), csr.indptr.data_ptr(),
+                                         csr.indices.data_ptr(), u_dev.data_ptr(), len(users),
+                                         _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
+                                         out.data_ptr(), P, nan.data_ptr(), _capi.stream_handle(dev))
+    _capi.check(rc, "nais_score_catalog")
+    model._last_nan = nan
+    return out
+
+
+def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlon_mat=None,
+               ordered=True, stream=None):
+    """Top-k (ids int64 [len(users), k], scores f32) of every listed user over its complement
+    candidates, ordered (score desc, POI id asc). Raises like torch.topk when a user has fewer
+    than k candidates (validation.py:26)."""
+    dev = model._check_device()
+    csr = device_csr(train_matrix, dev)
+    P = model.embed_history.weight.shape[0]
+    if csr.shape[1] != P:
+        raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
+    users = np.asarray(list(users), dtype=np.int64)
+    if len(users) == 0:
+        return (torch.empty(0, k, dtype=torch.int64, device=dev),
+                torch.empty(0, k, dtype=torch.float32, device=dev))
+    if np.any(P - csr.hist_len[users] < k):
+        raise RuntimeError("selected index k out of range")       # torch.topk's error
+    order = lpt_order(users, csr.hist_len, P) if ordered else users
+    u_dev = torch.from_numpy(order.astype(np.int32)).to(dev)
+    reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
+    n = len(order)
+    ids = torch.empty(n, k, dtype=torch.int32, device=dev)
+    sc = torch.empty(n, k, dtype=torch.float32, device=dev)
+    counters = torch.zeros(2, dtype=torch.int32, device=dev)
+    lib = _capi.load()
+    prm = model.nais_params()
+    nbytes = lib.nais_score_topk_workspace_size(prm, n, k)
+    ws = _workspace(dev, nbytes)
+    st = stream if stream is not None else _capi.stream_handle(dev)
+    rc = lib.nais_score_topk(prm, csr.indptr.data_ptr(), csr.indices.data_ptr(), u_dev.data_ptr(),
+                             n, k, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm), None,
+                             ids.data_ptr(), sc.data_ptr(), counters[0:1].data_ptr(),
+                             counters[1:2].data_ptr(), ws.data_ptr(), ws.numel(), st)
+    _capi.check(rc, "nais_score_topk")
+    model._last_nan = counters[0:1]
+    if ordered:
+        inv = np.empty(n, dtype=np.int64)
+        pos = {int(u): i for i, u in enumerate(order)}
+        inv[:] = [pos[int(u)] for u in users]
+        inv_t = torch.from_numpy(inv).to(dev)
+        ids, sc = ids.index_select(0, inv_t), sc.index_select(0, inv_t)
+    return ids.to(torch.int64), sc

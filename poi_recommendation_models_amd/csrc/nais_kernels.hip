@@ -1,0 +1,871 @@
+// nais_kernels.hip -- MI355X (gfx950 / CDNA4) kernels + C-ABI for the NAIS scoring path.
+//
+// Reference semantics (muyeon-jo/POI_recommendation_models):
+//   attention_network  model.py:57-89 (basic), :144-180 (region), :246-297 (region_distance)
+//   mask               model.py:92-95      forward (NaN count + sigmoid) model.py:40-55
+//   full-catalog eval  validation.py:11-27, :38-55, :69-127 ; candidates batches.py:52-65
+//
+// Mapping onto CDNA4. For one (candidate c, history item j) pair the reference evaluates
+//   x = h_j (.) t_c ; z = ReLU(W1 x + b1) ; a_j = w2 . z ; e_j = exp(a_j) * [h_j != c]
+//   logit_c = sum_j e_j (h_j . t_c) / (sum_j e_j)^beta
+// The W1 x products for 32 candidates x 32 hidden units are one v_mfma_f32_32x32x2_f32 per
+// K=2 slice (exact fp32 -- a k-ordered fmaf chain, no reduced precision):
+//   A (32 x 2)  = W1[i][k]       constant per workgroup, staged once in LDS in fragment order
+//   B (2 x 32)  = x[k][c]        formed in VGPRs as t_c[k] * h_j[k]  (t_c lives in VGPRs,
+//                                h_j is an LDS broadcast read: every lane of a half reads
+//                                the same address)
+//   C (32 x 32) = b1[i] + W1 x   lane l holds candidate (l & 31), 16 hidden rows.
+// Lane half hh = l >> 5 owns input dims [hh*DH, hh*DH+DH) (DH = D/2); for the region variants
+// this is exactly the [item | region] concatenation of model.py:153,157. The ReLU, the w2 dot,
+// exp, the beta-smoothed accumulation and h_j . t_c all stay in registers (one xor-32 shuffle
+// joins the two lane halves), so nothing of size [b, n, d] or [b, n, H] ever exists in memory.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+
+#include "nais.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int WAVES = 8;                    // 512-thread workgroups
+constexpr int THREADS = WAVES * 64;
+constexpr int CAND_PER_BLOCK = WAVES * 32;  // one 32-candidate MFMA column tile per wave
+constexpr int JC = 64;                      // history rows staged in LDS per chunk
+constexpr int TOPK_THREADS = 1024;
+constexpr int MAX_K = 1024;
+constexpr int MAX_BATCH_USERS = 512;        // users scored per catalog launch
+
+struct DevParams {
+  const float* eh;
+  const float* et;
+  const float* er;
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* wd;  // dist_layer.weight [2,2] (region_distance)
+  const float* bd;  // dist_layer.bias [2]
+  int64_t P;
+  int32_t item_dim, region_dim, H, din;
+  float beta;
+};
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---------------------------------------------------------------------------------------------
+// Workgroup-constant operands: W1 in MFMA-A fragment order, b1/w2 in accumulator-row order.
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB, bool DIST>
+struct Consts {
+  static constexpr int A4 = HB * (DH / 4) * 64;  // float4 entries of the W1 image
+  static constexpr int ADIST = DIST ? HB * 64 : 0;
+  static constexpr int EPI = 2 * 2 * HB * 16;    // b1 then w2, each [hh][hb*16+r]
+  static constexpr size_t BYTES = size_t(A4) * 16 + size_t(ADIST) * 4 + size_t(EPI) * 4;
+};
+
+// hidden row held in accumulator register r of block hb by lane half hh (32x32 C layout)
+__device__ __forceinline__ int acc_row(int hb, int r, int hh) {
+  return hb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+}
+
+template <int DH, int HB, bool DIST>
+__device__ void stage_consts(const DevParams& p, float4* Aimg, float* Adist, float* Eimg, int tid) {
+  using C = Consts<DH, HB, DIST>;
+  constexpr int D = 2 * DH;
+  for (int f = tid; f < C::A4; f += THREADS) {
+    const int ln = f & 63, q = (f >> 6) % (DH / 4), hb = (f >> 6) / (DH / 4);
+    const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 4 * q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < p.H) {
+      const float* w = p.w1 + (int64_t)i * p.din + k0;
+      v = make_float4(w[0], w[1], w[2], w[3]);
+    }
+    Aimg[f] = v;
+  }
+  if (DIST) {
+    for (int f = tid; f < C::ADIST; f += THREADS) {
+      const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
+      Adist[f] = (i < p.H) ? p.w1[(int64_t)i * p.din + D + (ln >> 5)] : 0.f;
+    }
+  }
+  for (int f = tid; f < C::EPI; f += THREADS) {
+    const int which = f / (2 * HB * 16), rem = f % (2 * HB * 16);
+    const int hh = rem / (HB * 16), hr = rem % (HB * 16), hb = hr / 16, r = hr % 16;
+    const int i = acc_row(hb, r, hh);
+    Eimg[f] = (i < p.H) ? (which == 0 ? p.b1[i] : p.w2[i]) : 0.f;
+  }
+}
+
+// One history item j against the lane's candidate: returns a_j (attn_layer2 output) and
+// s_j = h_j . t_c, both already combined across the two lane halves.
+//   hrow: this lane-half's DH floats of h_j (LDS broadcast or per-lane global)
+template <int DH, int HB, bool DIST, typename HPtr, typename EpiT>
+__device__ __forceinline__ void item_step(const float4 (&t4)[DH / 4], HPtr hrow,
+                                          const float4* __restrict__ Aimg,
+                                          const float* __restrict__ Adist, const EpiT& epi,
+                                          float distf, int lane, float& a_out, float& s_out) {
+  floatx16 acc[HB];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[hb][r] = epi.bias(hb * 16 + r);
+  float sd = 0.f;
+  // Software pipeline over the DH/4 k-groups: the LDS operands of group q+1 are requested before
+  // the 4*HB MFMAs of group q issue; sched_barrier keeps the compiler from hoisting every load of
+  // the item to the top (which costs ~HB*DH VGPRs and spills at D = H = 128).
+  float4 hv_n = *reinterpret_cast<const float4*>(hrow);
+  float4 a_n[HB];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) a_n[hb] = Aimg[(hb * (DH / 4)) * 64 + lane];
+#pragma unroll
+  for (int q = 0; q < DH / 4; ++q) {
+    const float4 hv = hv_n;
+    float4 a_c[HB];
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) a_c[hb] = a_n[hb];
+    if (q + 1 < DH / 4) {
+      hv_n = *reinterpret_cast<const float4*>(hrow + 4 * (q + 1));
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb) a_n[hb] = Aimg[(hb * (DH / 4) + q + 1) * 64 + lane];
+    }
+    const float x0 = t4[q].x * hv.x, x1 = t4[q].y * hv.y, x2 = t4[q].z * hv.z, x3 = t4[q].w * hv.w;
+    sd += x0;
+    sd += x1;
+    sd += x2;
+    sd += x3;
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+      acc[hb] = mfma32(a_c[hb].x, x0, acc[hb]);
+      acc[hb] = mfma32(a_c[hb].y, x1, acc[hb]);
+      acc[hb] = mfma32(a_c[hb].z, x2, acc[hb]);
+      acc[hb] = mfma32(a_c[hb].w, x3, acc[hb]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (DIST) {
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) acc[hb] = mfma32(Adist[hb * 64 + lane], distf, acc[hb]);
+  }
+  float ap = 0.f;
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = acc[hb][r];
+      const float z = (v < 0.f) ? 0.f : v;  // ReLU that keeps NaN, as torch.relu
+      ap = __builtin_fmaf(epi.w2(hb * 16 + r), z, ap);
+    }
+  a_out = ap + __shfl_xor(ap, 32);
+  s_out = sd + __shfl_xor(sd, 32);
+}
+
+// region_distance feature of one (c, j) pair for lane half hh (model.py:265; the pair's
+// (|dlat|, |dlng|) is formed in float64 and cast to float32 as at run.py:51-52 / validation.py:118)
+struct DistW {
+  float w0, w1, b;  // row hh of dist_layer: this lane half computes output feature hh
+};
+__device__ __forceinline__ DistW load_distw(const DevParams& p, int hh) {
+  return DistW{p.wd[2 * hh], p.wd[2 * hh + 1], p.bd[hh]};
+}
+__device__ __forceinline__ float dist_feature(const DistW& w, float ll0, float ll1) {
+  const float m0 = ll0 * 100.f, m1 = ll1 * 100.f;
+  return sigmoidf_ref(m0 * w.w0 + m1 * w.w1 + w.b);
+}
+
+// b1 / w2 for this lane half's accumulator rows: in VGPRs for H <= 64, else read from the LDS
+// image at each use (keeps H = 128 within the 256-VGPR budget of 2 waves per SIMD).
+template <int HB, bool REGS>
+struct Epi;
+template <int HB>
+struct Epi<HB, true> {
+  float b[HB * 16], w[HB * 16];
+  __device__ __forceinline__ void load(const float* Eimg, int hh) {
+#pragma unroll
+    for (int i = 0; i < HB * 16; ++i) {
+      b[i] = Eimg[hh * HB * 16 + i];
+      w[i] = Eimg[2 * HB * 16 + hh * HB * 16 + i];
+    }
+  }
+  __device__ __forceinline__ float bias(int i) const { return b[i]; }
+  __device__ __forceinline__ float w2(int i) const { return w[i]; }
+};
+template <int HB>
+struct Epi<HB, false> {
+  const float* pb;
+  const float* pw;
+  __device__ __forceinline__ void load(const float* Eimg, int hh) {
+    pb = Eimg + hh * HB * 16;
+    pw = Eimg + 2 * HB * 16 + hh * HB * 16;
+  }
+  __device__ __forceinline__ float bias(int i) const { return pb[i]; }
+  __device__ __forceinline__ float w2(int i) const { return pw[i]; }
+};
+
+__device__ __forceinline__ float finish_logit(float S, float N, float beta, bool empty) {
+  if (empty) return 0.f;  // sum over an empty history dim (model.py:79-88 with n == 0)
+  const float den = (beta == 0.5f) ? sqrtf(S) : powf(S, beta);
+  return N / den;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Full-catalog scoring: grid (ceil(P / 256), users in batch). Each workgroup = one user x 256
+// consecutive POI ids; the user's history rows are staged into LDS once per 64-row chunk and
+// broadcast to all 8 waves. Scores of history POIs are written as -1 (excluded from top-k).
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB, int VAR>
+__global__ void __launch_bounds__(THREADS, 1)
+catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
+                     const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                     const int64_t* __restrict__ region_of, const double* __restrict__ coords,
+                     const double* __restrict__ latlon_mat, float* __restrict__ scores,
+                     int64_t score_ld, int32_t* __restrict__ nan_count) {
+  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr int D = 2 * DH;
+  using C = Consts<DH, HB, DIST>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* Aimg = reinterpret_cast<float4*>(smem);
+  float* Adist = reinterpret_cast<float*>(Aimg + C::A4);
+  float* Eimg = Adist + C::ADIST;
+  float* hrows = Eimg + C::EPI;
+  int32_t* hid = reinterpret_cast<int32_t*>(hrows + JC * D);
+  double* hco = reinterpret_cast<double*>(hid + JC);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int64_t u = users[blockIdx.y];
+  const int64_t hbeg = indptr[u];
+  const int64_t hlen = indptr[u + 1] - hbeg;
+  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P;
+  const int64_t cc = valid ? c : p.P - 1;
+
+  stage_consts<DH, HB, DIST>(p, Aimg, Adist, Eimg, tid);
+
+  // candidate operand: t_c (this lane half's DH dims) in VGPRs for the whole history sweep
+  float4 t4[DH / 4];
+  {
+    const float* src = (REGION && hh) ? p.er + region_of[cc] * p.region_dim
+                                      : p.et + cc * p.item_dim + (REGION ? 0 : hh * DH);
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) t4[q] = reinterpret_cast<const float4*>(src)[q];
+  }
+  double clat = 0.0, clon = 0.0;
+  DistW dw{0.f, 0.f, 0.f};
+  const double* llrow = nullptr;  // latlon_mat row of this candidate (matrix mode)
+  if (DIST) {
+    if (coords) {
+      clat = coords[2 * cc];
+      clon = coords[2 * cc + 1];
+    } else {
+      llrow = latlon_mat + cc * p.P * 2;
+    }
+    dw = load_distw(p, hh);
+  }
+
+  float S = 0.f, N = 0.f;
+  bool in_hist = false;
+  Epi<HB, (HB <= 2 && DH <= 32)> epi;
+  __syncthreads();
+  epi.load(Eimg, hh);
+
+  for (int64_t j0 = 0; j0 < hlen; j0 += JC) {
+    const int jn = (int)std::min<int64_t>(JC, hlen - j0);
+    __syncthreads();  // consumers of the previous chunk are done
+    for (int f = tid; f < jn * (D / 4); f += THREADS) {
+      const int jj = f / (D / 4), q4 = f % (D / 4);
+      const int64_t item = indices[hbeg + j0 + jj];
+      float4 v;
+      if (!REGION || q4 < DH / 4)
+        v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
+      else
+        v = reinterpret_cast<const float4*>(p.er + region_of[item] * p.region_dim)[q4 - DH / 4];
+      reinterpret_cast<float4*>(hrows)[f] = v;
+    }
+    for (int jj = tid; jj < jn; jj += THREADS) {
+      const int64_t item = indices[hbeg + j0 + jj];
+      hid[jj] = (int32_t)item;
+      if (DIST && coords) {
+        hco[2 * jj] = coords[2 * item];
+        hco[2 * jj + 1] = coords[2 * item + 1];
+      }
+    }
+    __syncthreads();
+    for (int jj = 0; jj < jn; ++jj) {
+      float distf = 0.f;
+      if (DIST) {
+        float ll0, ll1;
+        if (coords) {
+          ll0 = (float)fabs(clat - hco[2 * jj]);
+          ll1 = (float)fabs(clon - hco[2 * jj + 1]);
+        } else {
+          ll0 = (float)llrow[2 * (int64_t)hid[jj]];
+          ll1 = (float)llrow[2 * (int64_t)hid[jj] + 1];
+        }
+        distf = dist_feature(dw, ll0, ll1);
+      }
+      float a, s;
+      item_step<DH, HB, DIST>(t4, hrows + jj * D + hh * DH, Aimg, Adist, epi, distf, lane, a, s);
+      const bool keep = hid[jj] != (int32_t)c;             // model.py:92-95
+      const float e = expf(a) * (keep ? 1.f : 0.f);        // model.py:75-78 (inf * 0 -> NaN)
+      in_hist |= !keep;
+      S += e;                                               // model.py:79
+      N += e * s;                                           // sum_j w_j (h_j . t) numerator
+    }
+  }
+
+  const float logit = finish_logit(S, N, p.beta, hlen == 0);
+  const bool isnan_ = logit != logit;
+  float sc = sigmoidf_ref(logit);
+  if (isnan_) sc = __builtin_nanf("");
+  if (in_hist) sc = -1.f;  // history POI: not a candidate (batches.py:56)
+  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (nan_count) {
+    const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
+    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// General forward: arbitrary per-row histories; each lane gathers its own row's h_j from
+// global memory (L2/MALL-resident tables), one item ahead of the MFMA sweep.
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB, int VAR>
+__global__ void __launch_bounds__(THREADS, 1)
+forward_kernel(DevParams p, const int64_t* __restrict__ hist, int64_t b, int64_t n, int64_t hist_ld,
+               const int64_t* __restrict__ target, const int64_t* __restrict__ hist_region,
+               int64_t hreg_ld, const int64_t* __restrict__ target_region,
+               const float* __restrict__ latlon, int64_t ll_ld, float* __restrict__ out,
+               int32_t* __restrict__ nan_count, int32_t flags) {
+  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  using C = Consts<DH, HB, DIST>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* Aimg = reinterpret_cast<float4*>(smem);
+  float* Adist = reinterpret_cast<float*>(Aimg + C::A4);
+  float* Eimg = Adist + C::ADIST;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int64_t r = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = r < b;
+  const int64_t rr = valid ? r : b - 1;
+  stage_consts<DH, HB, DIST>(p, Aimg, Adist, Eimg, tid);
+
+  const int64_t tgt = target[rr];
+  float4 t4[DH / 4];
+  {
+    const float* src = (REGION && hh) ? p.er + target_region[rr] * p.region_dim
+                                      : p.et + tgt * p.item_dim + (REGION ? 0 : hh * DH);
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) t4[q] = reinterpret_cast<const float4*>(src)[q];
+  }
+  const int64_t* hrow_ids = hist + rr * hist_ld;
+  DistW dw{0.f, 0.f, 0.f};
+  if (DIST) dw = load_distw(p, hh);
+  auto row_ptr = [&](int64_t j) -> const float* {
+    const int64_t item = hrow_ids[j];
+    if (REGION && hh) return p.er + hist_region[rr * hreg_ld + j] * p.region_dim;
+    return p.eh + item * p.item_dim + (REGION ? 0 : hh * DH);
+  };
+
+  Epi<HB, (HB <= 2 && DH <= 32)> epi;
+  __syncthreads();
+  epi.load(Eimg, hh);
+
+  float S = 0.f, N = 0.f;
+  constexpr bool PREFETCH = DH <= 32;  // one-item-ahead gather; at D = 128 it would spill
+  float4 hcur[DH / 4];
+  if (PREFETCH && n > 0) {
+    const float* hp = row_ptr(0);
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) hcur[q] = reinterpret_cast<const float4*>(hp)[q];
+  }
+  for (int64_t j = 0; j < n; ++j) {
+    float4 hnext[DH / 4];
+    if (!PREFETCH) {
+      const float* hp = row_ptr(j);
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) hcur[q] = reinterpret_cast<const float4*>(hp)[q];
+    } else if (j + 1 < n) {
+      const float* hp = row_ptr(j + 1);
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) hnext[q] = reinterpret_cast<const float4*>(hp)[q];
+    }
+    float distf = 0.f;
+    if (DIST) {
+      const float* ll = latlon + rr * ll_ld + 2 * j;
+      distf = dist_feature(dw, ll[0], ll[1]);
+    }
+    float a, s;
+    item_step<DH, HB, DIST>(t4, reinterpret_cast<const float*>(hcur), Aimg, Adist, epi, distf,
+                            lane, a, s);
+    const bool keep = hrow_ids[j] != tgt;
+    const float e = expf(a) * (keep ? 1.f : 0.f);
+    S += e;
+    N += e * s;
+    if (PREFETCH && j + 1 < n) {
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) hcur[q] = hnext[q];
+    }
+  }
+  const float logit = finish_logit(S, N, p.beta, n == 0);
+  const bool isnan_ = logit != logit;
+  float o = (flags & NAIS_FLAG_SIGMOID) ? sigmoidf_ref(logit) : logit;
+  if (valid && hh == 0) out[r] = o;
+  if (nan_count) {
+    const unsigned long long m = __ballot(valid && hh == 0 && isnan_);
+    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Top-k per user (validation.py:26-27): exact radix select on 64-bit keys
+//   key = ordered(score) << 32 | (0xFFFFFFFF - poi)   -> unique; larger key = (higher score, lower id)
+// 8 MSB-first 8-bit passes over the user's score row (L2-resident), then the k winners are
+// collected and bitonic-sorted in LDS. NaN (canonical, positive) orders above +inf.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ord_f32(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+__global__ void __launch_bounds__(TOPK_THREADS)
+topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k,
+            int32_t* __restrict__ out_ids, float* __restrict__ out_scores,
+            int32_t* __restrict__ short_count) {
+  __shared__ uint32_t hist[256];
+  __shared__ unsigned long long buf[MAX_K];
+  __shared__ uint32_t sh_bin, sh_above, sh_total, sh_cnt;
+  const float* s = scores + (int64_t)blockIdx.x * score_ld;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long prefix = 0, mask = 0;
+  uint32_t rem = (uint32_t)k;
+  int kk = k;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
+      float v = s[c];
+      if (v < 0.f) continue;  // history POI (or padding): not a candidate
+      const unsigned long long key =
+          ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)c);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int base = 255 - lane * 4;
+      const uint32_t c0 = hist[base], c1 = hist[base - 1], c2 = hist[base - 2], c3 = hist[base - 3];
+      const uint32_t local = c0 + c1 + c2 + c3;
+      uint32_t incl = local;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      if (pass == 0 && lane == 0) sh_total = total;
+      uint32_t need = rem;
+      if (pass == 0 && total < need) need = total;  // fewer candidates than k
+      const uint32_t excl = incl - local;
+      if (need > 0 && excl < need && incl >= need) {
+        uint32_t cum = excl;
+        int bsel;
+        if (cum + c0 >= need) bsel = base;
+        else if ((cum += c0) + c1 >= need) bsel = base - 1;
+        else if ((cum += c1) + c2 >= need) bsel = base - 2;
+        else { cum += c2; bsel = base - 3; }
+        sh_bin = (uint32_t)bsel;
+        sh_above = cum;
+      }
+      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; }
+    }
+    __syncthreads();
+    if (pass == 0) {
+      if (sh_total < (uint32_t)kk) kk = (int)sh_total;
+      rem = (uint32_t)kk;
+    }
+    prefix |= (unsigned long long)sh_bin << shift;
+    mask |= 255ull << shift;
+    rem -= sh_above;
+    __syncthreads();
+  }
+  if (tid == 0) sh_cnt = 0;
+  __syncthreads();
+  if (kk > 0) {
+    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
+      float v = s[c];
+      if (v < 0.f) continue;
+      const unsigned long long key =
+          ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)c);
+      if (key >= prefix) {
+        const uint32_t pos = atomicAdd(&sh_cnt, 1u);
+        if (pos < (uint32_t)MAX_K) buf[pos] = key;
+      }
+    }
+  }
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < k) n2 <<= 1;
+  for (int i = tid; i < n2; i += TOPK_THREADS)
+    if (i >= kk) buf[i] = 0ull;
+  __syncthreads();
+  // bitonic sort, descending
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2; i += TOPK_THREADS) {
+        const int partner = i ^ stride;
+        if (partner > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long x = buf[i], y = buf[partner];
+          if (desc ? (x < y) : (x > y)) {
+            buf[i] = y;
+            buf[partner] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += TOPK_THREADS) {
+    int32_t id = -1;
+    float sc = __builtin_nanf("");
+    if (i < kk) {
+      const unsigned long long key = buf[i];
+      id = (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+      sc = unord_f32((uint32_t)(key >> 32));
+    }
+    out_ids[(int64_t)blockIdx.x * k + i] = id;
+    out_scores[(int64_t)blockIdx.x * k + i] = sc;
+  }
+  if (tid == 0 && kk < k && short_count) atomicAdd(short_count, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Standalone row gather (HBM roofline kernel): 16 B per lane, one row per dim/4 lanes.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+gather_rows_kernel(const float4* __restrict__ table, int q4, const int64_t* __restrict__ idx,
+                   int64_t m, float4* __restrict__ out) {
+  const int64_t total = m * q4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / q4;
+    const int q = (int)(i - row * q4);
+    out[i] = table[idx[row] * q4 + q];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+gather_rows_scalar_kernel(const float* __restrict__ table, int dim, const int64_t* __restrict__ idx,
+                          int64_t m, float* __restrict__ out) {
+  const int64_t total = m * dim;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / dim;
+    out[i] = table[idx[row] * dim + (i - row * dim)];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NAIS_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return NAIS_OK;
+}
+
+struct Shape {
+  int DH, HB;
+};
+
+int validate(const nais_params_t* p, Shape* sh) {
+  if (!p) return fail(NAIS_E_INVALID, "params is NULL");
+  if (p->variant < 0 || p->variant > 2) return fail(NAIS_E_INVALID, "unknown variant");
+  if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
+    return fail(NAIS_E_INVALID, "missing parameter pointer");
+  if (p->num_pois <= 0) return fail(NAIS_E_INVALID, "num_pois must be > 0");
+  const int D = p->embed_dim;
+  if (D <= 0 || D % 8 != 0 || D > 128)
+    return fail(NAIS_E_UNSUPPORTED, "embed_dim must be a multiple of 8 in [8, 128]");
+  if (p->hidden <= 0 || p->hidden > 128) return fail(NAIS_E_UNSUPPORTED, "hidden must be in [1, 128]");
+  if (p->variant == NAIS_VARIANT_BASIC) {
+    if (p->item_dim != D || p->din != D) return fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
+  } else {
+    if (p->item_dim != D / 2 || p->region_dim != D / 2)
+      return fail(NAIS_E_INVALID, "region variants: item_dim == region_dim == embed_dim/2");
+    if (!p->embed_region || p->num_regions <= 0) return fail(NAIS_E_INVALID, "missing embed_region");
+    const int want = D + (p->variant == NAIS_VARIANT_REGION_DISTANCE ? 2 : 0);
+    if (p->din != want) return fail(NAIS_E_INVALID, "din mismatch for variant");
+    if (p->variant == NAIS_VARIANT_REGION_DISTANCE && (!p->dist_w || !p->dist_b))
+      return fail(NAIS_E_INVALID, "region_distance needs dist_layer weight and bias");
+  }
+  sh->DH = D / 2;
+  int hb = (p->hidden + 31) / 32;
+  if (hb == 3) hb = 4;
+  sh->HB = hb;
+  if (sh->DH != 4 && sh->DH != 8 && sh->DH != 16 && sh->DH != 32 && sh->DH != 64)
+    return fail(NAIS_E_UNSUPPORTED, "embed_dim must be one of 8, 16, 32, 64, 128");
+  return NAIS_OK;
+}
+
+int to_dev(const nais_params_t* p, DevParams* d) {
+  d->eh = p->embed_history;
+  d->et = p->embed_target;
+  d->er = p->embed_region;
+  d->w1 = p->w1;
+  d->b1 = p->b1;
+  d->w2 = p->w2;
+  d->P = p->num_pois;
+  d->item_dim = p->item_dim;
+  d->region_dim = p->region_dim;
+  d->H = p->hidden;
+  d->din = p->din;
+  d->beta = p->beta;
+  d->wd = p->dist_w;
+  d->bd = p->dist_b;
+  return NAIS_OK;
+}
+
+template <int DH, int HB, int VAR>
+size_t catalog_lds() {
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  return Consts<DH, HB, DIST>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
+         (DIST ? size_t(JC) * 16 : 0);
+}
+
+template <int DH, int HB, int VAR>
+int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* indices,
+                   const int32_t* users, int nb, const int64_t* region_of, const double* coords,
+                   const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
+                   hipStream_t stream) {
+  const size_t lds = catalog_lds<DH, HB, VAR>();
+  auto kern = catalog_score_kernel<DH, HB, VAR>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+  hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
+                     coords, latlon_mat, scores, ld, nan_count);
+  return check_launch("catalog_score_kernel");
+}
+
+template <int DH, int HB, int VAR>
+int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n, int64_t hist_ld,
+                   const int64_t* target, const int64_t* hreg, int64_t hreg_ld, const int64_t* treg,
+                   const float* latlon, int64_t ll_ld, float* out, int32_t* nan_count, int32_t flags,
+                   hipStream_t stream) {
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  const size_t lds = Consts<DH, HB, DIST>::BYTES;
+  auto kern = forward_kernel<DH, HB, VAR>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid((unsigned)((b + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK));
+  hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, hist, b, n, hist_ld, target, hreg,
+                     hreg_ld, treg, latlon, ll_ld, out, nan_count, flags);
+  return check_launch("forward_kernel");
+}
+
+// (DH, HB, VAR) -> template instance
+#define NAIS_DISPATCH(FN, DH_, HB_, VAR_, ...)                                   \
+  do {                                                                            \
+    switch (VAR_) {                                                               \
+      case 0: NAIS_DISPATCH_DH(FN, DH_, HB_, 0, __VA_ARGS__); break;              \
+      case 1: NAIS_DISPATCH_DH(FN, DH_, HB_, 1, __VA_ARGS__); break;              \
+      default: NAIS_DISPATCH_DH(FN, DH_, HB_, 2, __VA_ARGS__); break;             \
+    }                                                                             \
+  } while (0)
+#define NAIS_DISPATCH_DH(FN, DH_, HB_, V, ...)                                   \
+  switch (DH_) {                                                                  \
+    case 4: NAIS_DISPATCH_HB(FN, 4, HB_, V, __VA_ARGS__); break;                  \
+    case 8: NAIS_DISPATCH_HB(FN, 8, HB_, V, __VA_ARGS__); break;                  \
+    case 16: NAIS_DISPATCH_HB(FN, 16, HB_, V, __VA_ARGS__); break;                \
+    case 32: NAIS_DISPATCH_HB(FN, 32, HB_, V, __VA_ARGS__); break;                \
+    default: NAIS_DISPATCH_HB(FN, 64, HB_, V, __VA_ARGS__); break;                \
+  }
+#define NAIS_DISPATCH_HB(FN, DH, HB_, V, ...)                                    \
+  switch (HB_) {                                                                  \
+    case 1: rc = FN<DH, 1, V>(__VA_ARGS__); break;                                \
+    case 2: rc = FN<DH, 2, V>(__VA_ARGS__); break;                                \
+    default: rc = FN<DH, 4, V>(__VA_ARGS__); break;                               \
+  }
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t nais_abi_version(void) { return NAIS_ABI_VERSION; }
+
+const char* nais_last_error(void) { return g_err.c_str(); }
+
+int32_t nais_forward(const nais_params_t* params, const int64_t* hist, int64_t b, int64_t n,
+                     int64_t hist_ld, const int64_t* target, const int64_t* hist_region,
+                     int64_t hist_region_ld, const int64_t* target_region,
+                     const float* target_lat_long, int64_t latlon_ld, float* out,
+                     int32_t* nan_count, int32_t flags, void* stream) {
+  Shape sh;
+  int rc = validate(params, &sh);
+  if (rc) return rc;
+  if (b < 0 || n < 0) return fail(NAIS_E_INVALID, "negative b or n");
+  if (b == 0) return NAIS_OK;
+  if (!target || !out || (n > 0 && !hist)) return fail(NAIS_E_INVALID, "missing hist/target/out");
+  if (params->variant != NAIS_VARIANT_BASIC && (!target_region || (n > 0 && !hist_region)))
+    return fail(NAIS_E_INVALID, "region variants need hist_region and target_region");
+  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && n > 0 && !target_lat_long)
+    return fail(NAIS_E_INVALID, "region_distance needs target_lat_long");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DevParams d;
+  rc = to_dev(params, &d);
+  if (rc) return rc;
+  NAIS_DISPATCH(launch_forward, sh.DH, sh.HB, params->variant, d, hist, b, n, hist_ld, target,
+                hist_region, hist_region_ld, target_region, target_lat_long, latlon_ld, out,
+                nan_count, flags, st);
+  return rc;
+}
+
+size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k) {
+  (void)k;
+  if (!params || num_users <= 0) return 0;
+  const int64_t nb = std::min<int64_t>(num_users, MAX_BATCH_USERS);
+  return (size_t)(nb * round_up(params->num_pois, 64) * (int64_t)sizeof(float));
+}
+
+int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, const int64_t* indices,
+                        const int32_t* users, int32_t num_users, int32_t k,
+                        const int64_t* region_of, const double* coords,
+                        const double* latlon_mat, const nais_prior_t* prior,
+                        int32_t* out_ids, float* out_scores, int32_t* nan_count,
+                        int32_t* short_count, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+  Shape sh;
+  int rc = validate(params, &sh);
+  if (rc) return rc;
+  if (num_users < 0) return fail(NAIS_E_INVALID, "num_users < 0");
+  if (num_users == 0) return NAIS_OK;
+  if (k <= 0 || k > MAX_K) return fail(NAIS_E_UNSUPPORTED, "k must be in [1, 1024]");
+  if (!indptr || !indices || !users || !out_ids || !out_scores)
+    return fail(NAIS_E_INVALID, "missing indptr/indices/users/outputs");
+  if (params->variant != NAIS_VARIANT_BASIC && !region_of)
+    return fail(NAIS_E_INVALID, "region variants need region_of");
+  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && !coords && !latlon_mat)
+    return fail(NAIS_E_INVALID, "region_distance needs coords or latlon_mat");
+  if (prior) return fail(NAIS_E_UNSUPPORTED, "power-law prior epilogue is not in ABI v1");
+  const size_t need = nais_score_topk_workspace_size(params, num_users, k);
+  if (!workspace || workspace_bytes < need) return fail(NAIS_E_WORKSPACE, "workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DevParams d;
+  rc = to_dev(params, &d);
+  if (rc) return rc;
+  float* scores = reinterpret_cast<float*>(workspace);
+  const int64_t ld = round_up(params->num_pois, 64);
+  for (int32_t u0 = 0; u0 < num_users; u0 += MAX_BATCH_USERS) {
+    const int nb = std::min<int32_t>(MAX_BATCH_USERS, num_users - u0);
+    NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
+                  region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(topk_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld,
+                       params->num_pois, k, out_ids + (int64_t)u0 * k,
+                       out_scores + (int64_t)u0 * k, short_count);
+    rc = check_launch("topk_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,
+                           const int64_t* indices, const int32_t* users, int32_t num_users,
+                           const int64_t* region_of, const double* coords,
+                           const double* latlon_mat, float* scores, int64_t score_ld,
+                           int32_t* nan_count, void* stream) {
+  Shape sh;
+  int rc = validate(params, &sh);
+  if (rc) return rc;
+  if (num_users < 0) return fail(NAIS_E_INVALID, "num_users < 0");
+  if (num_users == 0) return NAIS_OK;
+  if (!indptr || !indices || !users || !scores) return fail(NAIS_E_INVALID, "missing pointer");
+  if (score_ld < params->num_pois) return fail(NAIS_E_INVALID, "score_ld < num_pois");
+  if (params->variant != NAIS_VARIANT_BASIC && !region_of)
+    return fail(NAIS_E_INVALID, "region variants need region_of");
+  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && !coords && !latlon_mat)
+    return fail(NAIS_E_INVALID, "region_distance needs coords or latlon_mat");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DevParams d;
+  rc = to_dev(params, &d);
+  if (rc) return rc;
+  for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_users - u0);
+    NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
+                  region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                  nan_count, st);
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, int32_t num_rows,
+                       int32_t k, int32_t* out_ids, float* out_scores, int32_t* short_count,
+                       void* stream) {
+  if (!scores || !out_ids || !out_scores || num_rows < 0 || num_pois <= 0 || score_ld < num_pois)
+    return fail(NAIS_E_INVALID, "bad topk_rows arguments");
+  if (k <= 0 || k > MAX_K) return fail(NAIS_E_UNSUPPORTED, "k must be in [1, 1024]");
+  if (num_pois > 0xFFFFFFFFll) return fail(NAIS_E_UNSUPPORTED, "num_pois must fit 32 bits");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int32_t r0 = 0; r0 < num_rows; r0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_rows - r0);
+    hipLaunchKernelGGL(topk_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores + (int64_t)r0 * score_ld,
+                       score_ld, num_pois, k, out_ids + (int64_t)r0 * k, out_scores + (int64_t)r0 * k,
+                       short_count);
+    const int rc = check_launch("topk_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim, const int64_t* idx,
+                         int64_t m, float* out, void* stream) {
+  if (!table || !idx || !out || rows <= 0 || dim <= 0 || m < 0)
+    return fail(NAIS_E_INVALID, "bad gather arguments");
+  if (m == 0) return NAIS_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = dim % 4 == 0 && (reinterpret_cast<uintptr_t>(table) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  const int64_t total = vec ? m * (dim / 4) : m * dim;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
+  if (vec)
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(table), dim / 4, idx, m,
+                       reinterpret_cast<float4*>(out));
+  else
+    hipLaunchKernelGGL(gather_rows_scalar_kernel, dim3((unsigned)blocks), dim3(256), 0, st, table,
+                       dim, idx, m, out);
+  return check_launch("gather_rows_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,233 @@
+"""Drop-in NAIS modules whose forward runs the gfx950 HIP kernels through the C-ABI.
+
+Constructor signatures, sub-module names (hence state_dict keys), initialisation and forward
+signatures follow the reference:
+
+* `NAIS_basic(item_num, embed_size, hidden_size, beta)`                               model.py:8-97
+* `NAIS_regionEmbedding(item_num, embed_size, hidden_size, beta, region_embed_size)`   model.py:99-187
+* `NAIS_region_distance_Embedding(item_num, embed_size, hidden_size, beta,
+                                  region_embed_size, dist_embed_size)`                model.py:189-304
+
+`forward` evaluates attention_network + sigmoid on the device in one fused kernel
+(`nais_forward`); there is no CPU path: inputs must live on the ROCm device that holds the
+parameters, otherwise a RuntimeError is raised. The modules implement eval-mode semantics
+(Dropout = identity, as under `model.eval()` in every reference validation loop). The training
+step (dropout + backward) is not built yet: forward in training mode raises.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _capi
+
+
+class _NAISDevice(nn.Module):
+    """Shared plumbing: parameter struct for the C-ABI, device checks, NaN reporting."""
+
+    VARIANT = _capi.VARIANT_BASIC
+    report_nan = True  # model.py:50-54 prints the NaN count of every forward
+
+    def _check_device(self, *tensors):
+        dev = self.embed_history.weight.device
+        if dev.type != "cuda":
+            raise RuntimeError(f"{type(self).__name__}: the NAIS path runs only on a ROCm device "
+                               f"(parameters are on {dev}); move the model with .to('cuda')")
+        for t in tensors:
+            if t is not None and t.device != dev:
+                raise RuntimeError(f"{type(self).__name__}: input on {t.device}, parameters on {dev}")
+        for n, p in self.named_parameters():
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise RuntimeError(f"{type(self).__name__}: parameter {n} must be contiguous float32")
+        return dev
+
+    def nais_params(self) -> _capi.NaisParams:
+        """`nais_params_t` view of this module's parameters (device pointers, no copies)."""
+        p = _capi.NaisParams()
+        p.variant = self.VARIANT
+        p.embed_dim = self.embed_size
+        p.item_dim = self.embed_history.weight.shape[1]
+        p.region_dim = self.embed_region.weight.shape[1] if hasattr(self, "embed_region") else 0
+        p.hidden = self.attn_layer1.weight.shape[0]
+        p.din = self.attn_layer1.weight.shape[1]
+        p.num_pois = self.embed_history.weight.shape[0]
+        p.num_regions = self.embed_region.weight.shape[0] if hasattr(self, "embed_region") else 0
+        p.beta = float(self.beta)
+        p.embed_history = self.embed_history.weight.data_ptr()
+        p.embed_target = self.embed_target.weight.data_ptr()
+        p.embed_region = self.embed_region.weight.data_ptr() if hasattr(self, "embed_region") else None
+        p.w1 = self.attn_layer1.weight.data_ptr()
+        p.b1 = self.attn_layer1.bias.data_ptr()
+        p.w2 = self.attn_layer2.weight.data_ptr()
+        if hasattr(self, "dist_layer"):
+            p.dist_w = self.dist_layer.weight.data_ptr()
+            p.dist_b = self.dist_layer.bias.data_ptr()
+        return p
+
+    def _run_forward(self, history, target, history_region=None, target_region=None,
+                     target_lat_long=None, sigmoid=True):
+        if self.training:
+            raise NotImplementedError(
+                f"{type(self).__name__}: training-mode forward (dropout + backward, SURVEY.md 8(f1)) "
+                "is not implemented on the HIP path yet; call model.eval()")
+        dev = self._check_device(history, target, history_region, target_region, target_lat_long)
+        if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
+            raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
+                             f"{tuple(target.shape)}")
+
+        def idx(t):
+            t = t.to(torch.int64)
+            return t if t.dim() < 2 or t.stride(1) == 1 else t.contiguous()
+
+        history, target = idx(history), idx(target).contiguous()
+        b, n = history.shape
+        ll, ll_ld = None, 0
+        if self.VARIANT != _capi.VARIANT_BASIC:
+            if history_region is None or target_region is None:
+                raise ValueError("region variants need history_region and target_region")
+            history_region = idx(history_region)
+            target_region = idx(target_region).contiguous()
+            if tuple(history_region.shape) != (b, n) or tuple(target_region.shape) != (b,):
+                raise ValueError("history_region must be [b, n] and target_region [b]")
+        if self.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+            if target_lat_long is None or tuple(target_lat_long.shape) != (b, n, 2):
+                raise ValueError("target_lat_long must be [b, n, 2]")
+            ll = target_lat_long.to(torch.float32)
+            if not (ll.stride(2) == 1 and ll.stride(1) == 2):
+                ll = ll.contiguous()
+            ll_ld = ll.stride(0)
+        out = torch.empty(b, dtype=torch.float32, device=dev)
+        nan = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _capi.load()
+        prm = self.nais_params()
+        rc = lib.nais_forward(prm, _capi.ptr(history) if n > 0 else None, b, n,
+                              history.stride(0) if n > 0 else 0, _capi.ptr(target),
+                              _capi.ptr(history_region) if (history_region is not None and n > 0) else None,
+                              history_region.stride(0) if (history_region is not None and n > 0) else 0,
+                              _capi.ptr(target_region), _capi.ptr(ll) if n > 0 else None, ll_ld,
+                              out.data_ptr(), nan.data_ptr(),
+                              _capi.FLAG_SIGMOID if sigmoid else 0, _capi.stream_handle(dev))
+        _capi.check(rc, "nais_forward")
+        self._last_nan = nan
+        if self.report_nan and isinstance(self, NAIS_basic):
+            c = int(nan.item())           # model.py:52 (.item() host sync, as in the reference)
+            if c > 0:
+                print(c)
+        return out
+
+    def get_mask(self, user_history, target_item):            # model.py:92-95
+        target_item = target_item.reshape([len(target_item), 1])
+        return user_history != target_item
+
+    def loss_function(self, prediction, label):              # model.py:96-97
+        return self.loss_func(prediction, label)
+
+
+class NAIS_basic(_NAISDevice):
+    VARIANT = _capi.VARIANT_BASIC
+
+    def __init__(self, item_num, embed_size, hidden_size, beta):
+        super().__init__()
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_history = nn.Embedding(item_num, self.embed_size)
+        self.embed_target = nn.Embedding(item_num, self.embed_size)
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = nn.BCELoss()
+        self.drop = nn.Dropout()
+        self.attn_layer1 = nn.Linear(self.embed_size, self.hidden_size)
+        self.attn_layer2 = nn.Linear(self.hidden_size, 1, bias=False)
+        self._init_weight_()
+
+    def _init_weight_(self):                                  # model.py:30-38
+        nn.init.normal_(self.embed_history.weight, std=0.01)
+        nn.init.normal_(self.embed_target.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def forward(self, history, target):                       # model.py:40-55
+        return self._run_forward(history, target)
+
+    def attention_network(self, user_history, target_item):   # model.py:57-89 (logits)
+        return self._run_forward(user_history, target_item, sigmoid=False)
+
+
+class NAIS_regionEmbedding(_NAISDevice):
+    VARIANT = _capi.VARIANT_REGION
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_history = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_target = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = nn.BCELoss()
+        self.attn_layer1 = nn.Linear(embed_size, hidden_size)
+        self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self.drop = nn.Dropout()
+        self._init_weight_()
+
+    def _init_weight_(self):                                  # model.py:121-130
+        nn.init.normal_(self.embed_history.weight, std=0.01)
+        nn.init.normal_(self.embed_target.weight, std=0.01)
+        nn.init.normal_(self.embed_region.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def forward(self, history, target, history_region, target_region):   # model.py:132-142
+        return self._run_forward(history, target, history_region, target_region)
+
+    def attention_network(self, user_history, target_item, history_region, target_region):
+        return self._run_forward(user_history, target_item, history_region, target_region,
+                                 sigmoid=False)
+
+
+class NAIS_region_distance_Embedding(_NAISDevice):
+    VARIANT = _capi.VARIANT_REGION_DISTANCE
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size, dist_embed_size):
+        super().__init__()
+        self.DEVICE = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_history = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_target = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self.embed_distance = nn.Embedding(dist_embed_size, embed_size)   # unused, as in model.py:204
+        self.relu = nn.ReLU()
+        self.tanh = nn.Tanh()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = nn.BCELoss()
+        self.attn_layer1 = nn.Linear(embed_size + 2, hidden_size)
+        self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self.dist_layer = nn.Linear(2, 2)
+        self._init_weight_()
+
+    def _init_weight_(self):                                  # model.py:219-229
+        nn.init.normal_(self.embed_history.weight, std=0.01)
+        nn.init.normal_(self.embed_target.weight, std=0.01)
+        nn.init.normal_(self.embed_region.weight, std=0.01)
+        nn.init.normal_(self.embed_distance.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def forward(self, history, target, history_region, target_region, target_lat_long):  # :231-244
+        return self._run_forward(history, target, history_region, target_region, target_lat_long)
+
+    def attention_network(self, user_history, target_item, history_region, target_region,
+                          target_lat_long_tensor):
+        return self._run_forward(user_history, target_item, history_region, target_region,
+                                 target_lat_long_tensor, sigmoid=False)

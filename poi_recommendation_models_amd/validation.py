@@ -1,0 +1,62 @@
+"""Drop-in evaluation loops (same signatures and 6-tuple result as validation.py:7-131).
+
+Each function scores every user's full catalog (complement of the training history) on the
+device with the fused NAIS kernel + radix-select top-k (`catalog.score_topk`), builds the same
+`recommended_list` (args.topk POI ids per user, best first) and returns
+(precision_v, recall_v, hit_v, precision_t, recall_t, hit_t) from `eval_metrics.evaluate_mp`.
+The model must be one of this package's NAIS modules, on a ROCm device.
+"""
+from __future__ import annotations
+
+from . import eval_metrics
+from .catalog import score_topk
+
+
+def recommend(model, args, num_users, train_matrix, **kw):
+    """recommended_list of validation.py:9-27: per user, args.topk POI ids, best first."""
+    model.eval()                                               # validation.py:8
+    ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
+    nan = int(model._last_nan.item())
+    if nan > 0:
+        print(nan)                                             # model.py:53-54
+    return ids.cpu().tolist()
+
+
+def _metrics(test_positive, val_positive, recommended_list, k_list):
+    precision_v, recall_v, hit_v = eval_metrics.evaluate_mp(val_positive, recommended_list, k_list)
+    precision_t, recall_t, hit_t = eval_metrics.evaluate_mp(test_positive, recommended_list, k_list)
+    return precision_v, recall_v, hit_v, precision_t, recall_t, hit_t
+
+
+def NAIS_validation(model, args, num_users, test_positive, val_positive, train_matrix, k_list):
+    """validation.py:7-31 (NAIS_basic)."""
+    rec = recommend(model, args, num_users, train_matrix)
+    return _metrics(test_positive, val_positive, rec, k_list)
+
+
+def NAIS_region_validation(model, args, num_users, test_positive, val_positive, train_matrix,
+                           businessRegionEmbedList, k_list):
+    """validation.py:34-59 (NAIS_regionEmbedding)."""
+    rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList)
+    return _metrics(test_positive, val_positive, rec, k_list)
+
+
+def NAIS_region_distance_validation(model, args, num_users, test_positive, val_positive,
+                                    train_matrix, businessRegionEmbedList, latlon_mat, k_list,
+                                    poi_coords=None):
+    """validation.py:62-131 (NAIS_region_distance_Embedding).
+
+    The reference reads (|dlat|, |dlng|) from a P x P x 2 float64 `latlon_mat` (run.py:47-54,214).
+    Pass `poi_coords` ([P, 2] lat/lng, the coordinates latlon_mat was built from) to have the
+    kernel form the same float64 differences on the fly instead -- bit-identical, and the only
+    option at P >= ~50k where the matrix does not fit. `latlon_mat=None` requires poi_coords.
+    `args.powerlaw_weight` is read but unused, as at validation.py:66.
+    """
+    _ = args.powerlaw_weight
+    if poi_coords is not None:
+        rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
+                        coords=poi_coords)
+    else:
+        rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
+                        latlon_mat=latlon_mat)
+    return _metrics(test_positive, val_positive, rec, k_list)
