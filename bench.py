@@ -15,7 +15,6 @@ Per-GPU work per step is fixed -> weak scaling.
 from __future__ import annotations
 
 import argparse
-import heapq
 import json
 import os
 import sys
@@ -46,19 +45,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
-
-
-def shard_users(hist_len, P, world):
-    """LPT: heaviest user to the least-loaded rank (SURVEY.md 8(e) partitioning)."""
-    cost = (P - hist_len) * hist_len
-    order = np.argsort(-cost, kind="stable")
-    heap = [(0, r) for r in range(world)]
-    out = [[] for _ in range(world)]
-    for u in order:
-        load, r = heapq.heappop(heap)
-        out[r].append(int(u))
-        heapq.heappush(heap, (load + int(cost[u]), r))
-    return [np.array(x, dtype=np.int64) for x in out]
 
 
 def cpu_baseline(p, data, users, k, seconds):
@@ -99,6 +85,7 @@ def main():
     from poi_recommendation_models_amd import _capi
     from poi_recommendation_models_amd.catalog import DeviceCSR
     from poi_recommendation_models_amd.model import NAIS_basic
+    from poi_recommendation_models_amd.sharding import broadcast_module, shard_users
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
 
     P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
@@ -111,8 +98,7 @@ def main():
     model = model.to(dev).eval()
     model.report_nan = False
     if world > 1:   # replicate the POI tables + MLP over RCCL (xGMI), once
-        for t in model.state_dict().values():
-            dist.broadcast(t, src=0)
+        broadcast_module(model, src=0)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
     hist_len = data.hist_len()
     mine = shard_users(hist_len, P, world)[rank]

@@ -1,0 +1,77 @@
+"""Multi-rank host logic on CPU (gloo, world_size 2): LPT user sharding and the top-k gather
+reassemble exactly the single-process recommended lists. The per-rank scorer here is the
+oracle (test infrastructure); on the GPUs it is catalog.score_topk."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import torch
+
+from _helpers import load_golden, params_from
+from oracle import nais_oracle
+from poi_recommendation_models_amd.sharding import gather_topk, shard_users
+
+
+def test_shard_users_lpt_balance():
+    rng = np.random.default_rng(0)
+    h = rng.integers(1, 201, 5000)
+    parts = shard_users(h, 100_000, 8)
+    allu = np.sort(np.concatenate(parts))
+    np.testing.assert_array_equal(allu, np.arange(5000))
+    cost = (100_000 - h) * h
+    loads = np.array([cost[p].sum() for p in parts])
+    assert loads.max() / loads.mean() < 1.001
+    assert [len(p) for p in shard_users(h[:3], 1000, 4)].count(0) == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = load_golden("catalog_basic.npz")
+    p = params_from(z, "trained")
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    hl = np.diff(z["indptr"])
+    mine = shard_users(hl, P, world)[rank]
+    ids, sc = [], []
+    for u in mine:
+        cand, s = nais_oracle.catalog_scores_basic(p, z["indices"][z["indptr"][u]:z["indptr"][u + 1]], P)
+        i, t = nais_oracle.topk_ids(cand, s, 50)
+        ids.append(i)
+        sc.append(t)
+    ids = torch.as_tensor(np.array(ids).reshape(-1, 50))
+    sc = torch.as_tensor(np.array(sc, dtype=np.float32).reshape(-1, 50))
+    gi, gs = gather_topk(mine, ids, sc, U)
+    q.put((rank, gi.numpy(), gs.numpy()))
+    dist.destroy_process_group()
+
+
+def test_gather_topk_world2_matches_single_process():
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    z = load_golden("catalog_basic.npz")
+    p = params_from(z, "trained")
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    ref = np.array([nais_oracle.topk_ids(*nais_oracle.catalog_scores_basic(
+        p, z["indices"][z["indptr"][u]:z["indptr"][u + 1]], P), 50)[0] for u in range(U)])
+    for rank, gi, gs in res:
+        np.testing.assert_array_equal(gi, ref)
+        assert not np.isnan(gs).any()
