@@ -27,6 +27,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense), spec
+PEAK_F16_MFMA_TFLOPS = 2500.0   # MI355X_MICROARCH.md: BF16/F16 MFMA dense peak, spec
+# the fp16x3 path issues 3 f16 MFMA products per algorithmic fp32 product, so its roof in
+# algorithmic (fp32-equivalent) FLOP/s is the f16 dense peak / 3
+PEAKS = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_F16_MFMA_TFLOPS / 3,
+         "fp16x3_pairsplit": PEAK_F16_MFMA_TFLOPS / 3}
 
 
 def parse():
@@ -41,6 +46,9 @@ def parse():
     ap.add_argument("--hidden", type=int, default=64)
     ap.add_argument("--h-max", type=int, default=200)
     ap.add_argument("--topk", type=int, default=50)
+    ap.add_argument("--precision", default="fp16x3", choices=["fp32", "fp16x3", "fp16x3_pairsplit"])
+    ap.add_argument("--no-fp32-leg", action="store_true",
+                    help="skip the extra exact-fp32 timing reported under 'fp32_path'")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -97,6 +105,7 @@ def main():
         model.load_state_dict({k: torch.from_numpy(v) for k, v in p_host.items()}, strict=False)
     model = model.to(dev).eval()
     model.report_nan = False
+    model.precision = a.precision
     if world > 1:   # replicate the POI tables + MLP over RCCL (xGMI), once
         broadcast_module(model, src=0)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
@@ -115,7 +124,6 @@ def main():
                       int((P - hist_len[us]).sum()),
                       int(((P - hist_len[us]) * hist_len[us]).sum())))
     lib = _capi.load()
-    prm = model.nais_params()
     scores = torch.empty(B, P, dtype=torch.float32, device=dev)
     ids = torch.empty(B, K, dtype=torch.int32, device=dev)
     top = torch.empty(B, K, dtype=torch.float32, device=dev)
@@ -125,40 +133,47 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step(s, ev=None):
-        u_dev = steps[s][0]
-        if ev is not None:
-            ev[0].record(stream)
-        _capi.check(lib.nais_score_catalog(prm, csr.indptr.data_ptr(), csr.indices.data_ptr(),
-                                           u_dev.data_ptr(), B, None, None, None, scores.data_ptr(),
-                                           P, cnt[0:1].data_ptr(), sh), "score_catalog")
-        if ev is not None:
-            ev[1].record(stream)
-        _capi.check(lib.nais_topk_rows(scores.data_ptr(), P, P, B, K, ids.data_ptr(), top.data_ptr(),
-                                       cnt[1:2].data_ptr(), sh), "topk_rows")
-        if ev is not None:
-            ev[2].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gat_ids, ids)
-            dist.all_gather_into_tensor(gat_sc, top)
+    def run(precision, nwarm, nsteps):
+        """nwarm untimed + nsteps timed steps; returns (elapsed s, catalog ms list, topk ms list)."""
+        model.precision = precision
+        prm = model.nais_params()
 
-    for s in range(a.warmup):
-        step(s)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i, evs[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+        def step(s, ev=None):
+            u_dev = steps[s][0]
+            if ev is not None:
+                ev[0].record(stream)
+            _capi.check(lib.nais_score_catalog(prm, csr.indptr.data_ptr(), csr.indices.data_ptr(),
+                                               u_dev.data_ptr(), B, None, None, None,
+                                               scores.data_ptr(), P, cnt[0:1].data_ptr(), sh),
+                        "score_catalog")
+            if ev is not None:
+                ev[1].record(stream)
+            _capi.check(lib.nais_topk_rows(scores.data_ptr(), P, P, B, K, ids.data_ptr(),
+                                           top.data_ptr(), cnt[1:2].data_ptr(), sh), "topk_rows")
+            if ev is not None:
+                ev[2].record(stream)
+            if world > 1:
+                dist.all_gather_into_tensor(gat_ids, ids)
+                dist.all_gather_into_tensor(gat_sc, top)
+
+        for s in range(nwarm):
+            step(s)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(nsteps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(nsteps):
+            step(nwarm + i, evs[i])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        return (el, [e[0].elapsed_time(e[1]) for e in evs], [e[1].elapsed_time(e[2]) for e in evs])
+
+    elapsed, score_ms, topk_ms = run(a.precision, a.warmup, a.steps)
     pairs = sum(steps[a.warmup + i][1] for i in range(a.steps))
     work = sum(steps[a.warmup + i][2] for i in range(a.steps))
-    score_ms = [evs[i][0].elapsed_time(evs[i][1]) for i in range(a.steps)]
-    topk_ms = [evs[i][1].elapsed_time(evs[i][2]) for i in range(a.steps)]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -173,13 +188,24 @@ def main():
     flops = work * flop_per_pair_item / a.steps          # algorithmic FLOP per catalog launch
     avg_score_s = float(np.mean(score_ms)) / 1e3
     achieved = flops / avg_score_s / 1e12
+    peak = PEAKS[a.precision]
     traffic = None
     try:
-        tj = json.load(open(a.traffic_json))
+        tj = json.load(open(a.traffic_json)).get(a.precision, {})
         if tj.get("users_per_launch") == B and tj.get("num_pois") == P and tj.get("dim") == D:
             traffic = tj.get("hbm_bytes_per_launch")
     except Exception:
         pass
+    fp32_leg = None
+    if world == 1 and not a.no_fp32_leg and a.precision != "fp32":
+        n32 = min(a.steps, 3)
+        el32, sm32, _ = run("fp32", 1, n32)
+        p32 = sum(steps[1 + i][1] for i in range(n32))
+        w32 = sum(steps[1 + i][2] for i in range(n32)) * flop_per_pair_item / n32
+        ach32 = w32 / (float(np.mean(sm32)) / 1e3) / 1e12
+        fp32_leg = {"precision": "fp32 (v_mfma_f32_32x32x2_f32, exact fp32)", "value": p32 / el32,
+                    "unit": "pairs/s", "steps": n32, "achieved": ach32, "peak": PEAK_FP32_MFMA_TFLOPS,
+                    "frac": ach32 / PEAK_FP32_MFMA_TFLOPS, "avg_launch_ms": float(np.mean(sm32))}
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
@@ -195,7 +221,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if a.precision == "fp32" else
+                     "fp32 (W1 x products as 3 fp16 MFMA products of power-of-two-scaled hi/lo splits, fp32 accumulate)",
             "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
             "config": {
                 "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
@@ -206,18 +233,22 @@ def main():
                 "parallelism": f"users sharded (LPT) over {world} GPU(s), POI tables replicated",
             },
             "roofline": {
-                "kernel": "catalog_score_kernel (nais_score_catalog)",
+                "kernel": ("catalog_score_kernel" if a.precision == "fp32" else
+                           "catalog_score_x3b_kernel") + " (nais_score_catalog)",
                 "bound": "mfma",
                 "achieved": achieved,
-                "peak": PEAK_FP32_MFMA_TFLOPS,
+                "peak": peak,
+                "peak_basis": ("fp32 MFMA dense" if a.precision == "fp32" else
+                               "f16 MFMA dense 2.5 PF / 3 products per algorithmic fp32 product"),
                 "unit": "TFLOP/s",
-                "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+                "frac": achieved / peak,
                 "traffic": traffic,
                 "algorithmic_flop_per_launch": flops,
                 "avg_launch_ms": avg_score_s * 1e3,
                 "topk_avg_launch_ms": float(np.mean(topk_ms)),
             },
             "cpu_baseline": cpu,
+            "fp32_path": fp32_leg,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

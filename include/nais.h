@@ -31,12 +31,20 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 1
+#define NAIS_ABI_VERSION 2
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
 #define NAIS_VARIANT_REGION 1          /* NAIS_regionEmbedding            model.py:99-187  */
 #define NAIS_VARIANT_REGION_DISTANCE 2 /* NAIS_region_distance_Embedding  model.py:189-304 */
+
+/* arithmetic of the W1 x products in the catalog scorer (nais_score_topk / nais_score_catalog) */
+#define NAIS_PRECISION_FP32 0          /* v_mfma_f32_32x32x2_f32: exact fp32 (k-ordered fmaf chain)           */
+#define NAIS_PRECISION_FP16X3 1        /* v_mfma_f32_32x32x16_f16 on power-of-two-scaled hi/lo fp16 splits:
+                                          3 products per fp32 product, fp32 accumulate, ~2^-21 relative;
+                                          operands A_j = W1 diag(h_j) (split once per item) and t_c     */
+#define NAIS_PRECISION_FP16X3_PAIRSPLIT 2 /* same arithmetic class, splitting x = h_j (.) t_c per pair
+                                          (the reference's operand order; more VALU work)                 */
 
 /* flags for nais_forward */
 #define NAIS_FLAG_SIGMOID 1            /* apply sigmoid (model.py:55); else return the logits of attention_network */
@@ -62,7 +70,7 @@ typedef struct nais_params {
   int64_t num_pois;             /* P = rows of embed_history / embed_target                            */
   int64_t num_regions;          /* R = rows of embed_region (0 for basic)                              */
   float beta;                   /* attention smoothing exponent (model.py:80), 0.5 in every driver     */
-  float _pad0;
+  int32_t precision;            /* NAIS_PRECISION_* (catalog scorer; nais_forward is always fp32)      */
   const float* embed_history;   /* embed_history.weight [P, item_dim]        model.py:15,106,198      */
   const float* embed_target;    /* embed_target.weight  [P, item_dim]        model.py:16,107,199      */
   const float* embed_region;    /* embed_region.weight  [R, region_dim]|NULL model.py:109,203         */

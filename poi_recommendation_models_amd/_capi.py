@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 1
+ABI_VERSION = 2
+PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE = 0, 1, 2
 FLAG_SIGMOID = 1
 
@@ -26,7 +27,7 @@ class NaisParams(ctypes.Structure):
         ("variant", ctypes.c_int32), ("embed_dim", ctypes.c_int32), ("item_dim", ctypes.c_int32),
         ("region_dim", ctypes.c_int32), ("hidden", ctypes.c_int32), ("din", ctypes.c_int32),
         ("num_pois", ctypes.c_int64), ("num_regions", ctypes.c_int64),
-        ("beta", ctypes.c_float), ("_pad0", ctypes.c_float),
+        ("beta", ctypes.c_float), ("precision", ctypes.c_int32),
         ("embed_history", ctypes.c_void_p), ("embed_target", ctypes.c_void_p),
         ("embed_region", ctypes.c_void_p), ("w1", ctypes.c_void_p), ("b1", ctypes.c_void_p),
         ("w2", ctypes.c_void_p), ("dist_w", ctypes.c_void_p), ("dist_b", ctypes.c_void_p),

@@ -23,7 +23,10 @@ def build(force=False, extra=()):
     deps = [SRC, os.path.join(ROOT, "include", "nais.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+    # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds/muls into v_pk_*_f32, which
+    # cost more issue slots than two scalar ops beside MFMAs (cdna_hip_programming.md, price table);
+    # measured +5 % on the split-fp16 catalog kernel (profiles/r1/ab_*.json).
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
            "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC, *extra]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

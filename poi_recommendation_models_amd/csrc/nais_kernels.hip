@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 
 #include "nais.h"
@@ -32,7 +33,13 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int WAVES = 8;                    // 512-thread workgroups
+#ifndef NAIS_WAVES
+#define NAIS_WAVES 8
+#endif
+#ifndef NAIS_X3B_SCHED
+#define NAIS_X3B_SCHED 0
+#endif
+constexpr int WAVES = NAIS_WAVES;           // 512-thread workgroups
 constexpr int THREADS = WAVES * 64;
 constexpr int CAND_PER_BLOCK = WAVES * 32;  // one 32-candidate MFMA column tile per wave
 constexpr int JC = 64;                      // history rows staged in LDS per chunk
@@ -426,6 +433,663 @@ forward_kernel(DevParams p, const int64_t* __restrict__ hist, int64_t b, int64_t
 }
 
 // ---------------------------------------------------------------------------------------------
+// Split-fp16 ("3xf16") catalog scorer: the same computation as catalog_score_kernel with the
+// W1 x products on v_mfma_f32_32x32x16_f16 (16x the f32-MFMA rate). Every fp32 operand v is
+// scaled by a power of two (exact) into fp16 range and split v = hi + lo, hi = f16(v),
+// lo = f16(v - hi) (22 significant bits together); the product is accumulated in fp32 as
+//   al*bh + ah*bl + ah*bh        (al*bl ~ 2^-22 relative is dropped),
+// i.e. ~2^-21 relative per product against fp32's 2^-24 -- scores stay within ~2e-7 of the
+// reference (tests/test_gpu_parity.py, both precisions). Scales:
+//   S_w = 2^e: max|W1[:, :D]| * S_w in [2^13, 2^14)   (per workgroup, from the LDS image)
+//   S_t = 2^e per candidate and history chunk: max|t_c| * max|h_chunk| * S_t in [2^13, 2^14),
+//         applied to t_c (so x_s = t_s * h_j = S_t * fl32(t_c * h_j) exactly).
+// b1 / w2 are pre-scaled per chunk so acc = S_w*S_t*(W1 x + b1) and a_j = sum w2/(S_w S_t) relu(acc).
+// ---------------------------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ floatx16 mfma16(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// 2^e with m * 2^e in [2^13, 2^14) for finite m > 0 (clamped), 1 otherwise
+__device__ __forceinline__ float pow2_scale(float m) {
+  if (!(m > 0.f) || !(m < __builtin_huge_valf())) return 1.f;
+  const uint32_t bits = __float_as_uint(m);
+  int ex = (int)((bits >> 23) & 255u) - 127;
+  if (((bits >> 23) & 255u) == 0u) ex = -127;  // subnormal product: maximal (clamped) scale
+  int e = 13 - ex;
+  e = e < -120 ? -120 : (e > 120 ? 120 : e);
+  return __uint_as_float((uint32_t)(e + 127) << 23);
+}
+
+// x -> (hi, lo): hi = f16(x) (RNE, v_cvt_pk_f16_f32), lo = f16(x - hi) with the subtraction done
+// exactly inside v_fma_mix{lo,hi}_f16 (one instruction per element instead of cvt + sub + cvt).
+// The trailing s_nop 1 covers the VALU-write -> MFMA-operand-read hazard that hipcc does not
+// pad for inline asm (cdna_hip_programming.md 5.7 item 2).
+__device__ __forceinline__ void split8(const float (&x)[8], half8& hi, half8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) hi[e] = (_Float16)x[e];
+  const uint4 hu = *reinterpret_cast<const uint4*>(&hi);
+  uint32_t l0, l1, l2, l3;
+  asm("v_fma_mixlo_f16 %0, -%4, 1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%4, 1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, -%5, 1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%5, 1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %2, -%6, 1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %2, -%6, 1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, -%7, 1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, -%7, 1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(hu.x), "v"(hu.y), "v"(hu.z), "v"(hu.w), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]),
+        "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]));
+  const uint4 lu = make_uint4(l0, l1, l2, l3);
+  lo = *reinterpret_cast<const half8*>(&lu);
+}
+
+__device__ float block_max(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float m = red[0];
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) m = fmaxf(m, red[w]);
+  return m;
+}
+
+template <int DH, int HB, bool DIST>
+struct Consts16 {
+  static constexpr int KS = DH / 8;                 // f16 MFMA K-steps (8 dims per lane half)
+  static constexpr int A16 = HB * KS * 2 * 64;      // uint4 entries: [hb][s][hi|lo][lane]
+  static constexpr int ADIST = DIST ? HB * 64 : 0;  // fp32 (S_w-scaled) distance columns
+  static constexpr int EPI = 2 * 2 * HB * 16;
+  static constexpr size_t BYTES = size_t(A16) * 16 + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64;
+};
+
+// ReLU as one signed-integer max on the float bits: negative floats (and -0, negative NaNs) are
+// negative int32 -> 0.0f; positive values and positive NaNs pass unchanged. One v_max_i32, no
+// canonicalising v_max_f32 on the MFMA result.
+__device__ __forceinline__ float relu_bits(float v) {
+  return __int_as_float(max(__float_as_int(v), 0));
+}
+
+template <int HB, bool REGS>
+struct Epi16;
+template <int HB>
+struct Epi16<HB, true> {           // pre-scaled copies in VGPRs: acc starts at S*b1
+  float bs[HB * 16], ws[HB * 16];
+  __device__ __forceinline__ void rescale(const float* Eimg, int hh, float S, float invS) {
+#pragma unroll
+    for (int i = 0; i < HB * 16; ++i) {
+      bs[i] = Eimg[hh * HB * 16 + i] * S;
+      ws[i] = Eimg[2 * HB * 16 + hh * HB * 16 + i] * invS;
+    }
+  }
+  __device__ __forceinline__ float init(int i) const { return bs[i]; }
+  __device__ __forceinline__ float term(int i, float acc, float) const {
+    return ws[i] * relu_bits(acc);
+  }
+};
+template <int HB>
+struct Epi16<HB, false> {          // b1 / w2 read from LDS: acc starts at 0, unscaled per use
+  const float* pb;
+  const float* pw;
+  __device__ __forceinline__ void rescale(const float* Eimg, int hh, float, float) {
+    pb = Eimg + hh * HB * 16;
+    pw = Eimg + 2 * HB * 16 + hh * HB * 16;
+  }
+  __device__ __forceinline__ float init(int) const { return 0.f; }
+  __device__ __forceinline__ float term(int i, float acc, float invS) const {
+    return pw[i] * relu_bits(__builtin_fmaf(acc, invS, pb[i]));
+  }
+};
+
+template <int DH, int HB, int VAR>
+__global__ void __launch_bounds__(THREADS, 1)
+catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
+                        const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                        const int64_t* __restrict__ region_of, const double* __restrict__ coords,
+                        const double* __restrict__ latlon_mat, float* __restrict__ scores,
+                        int64_t score_ld, int32_t* __restrict__ nan_count) {
+  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr int D = 2 * DH;
+  constexpr int KS = DH / 8;
+  constexpr bool EREGS = HB <= 2 && DH <= 32;
+  using C = Consts16<DH, HB, DIST>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* A16 = reinterpret_cast<uint4*>(smem);
+  float* Adist = reinterpret_cast<float*>(A16 + C::A16);
+  float* Eimg = Adist + C::ADIST;
+  float* red = Eimg + C::EPI;                        // 16 floats of reduction scratch
+  float* hrows = red + 16;
+  int32_t* hid = reinterpret_cast<int32_t*>(hrows + JC * D);
+  double* hco = reinterpret_cast<double*>(hid + JC);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int64_t u = users[blockIdx.y];
+  const int64_t hbeg = indptr[u];
+  const int64_t hlen = indptr[u + 1] - hbeg;
+  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P;
+  const int64_t cc = valid ? c : p.P - 1;
+
+  // ---- W1 scale, then the split A image (hi/lo per 8-dim slice) and the fp32 distance columns
+  float wmax = 0.f;
+  for (int f = tid; f < p.H * D; f += THREADS) {
+    const int i = f / D, k = f - i * D;
+    wmax = fmaxf(wmax, fabsf(p.w1[(int64_t)i * p.din + k]));
+  }
+  const float Sw = pow2_scale(block_max(wmax, red));
+  for (int f = tid; f < C::A16; f += THREADS) {
+    const int ln = f & 63, part = (f >> 6) & 1, s = ((f >> 7) % KS), hb = (f >> 7) / KS;
+    const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 8 * s;
+    half8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float w = (i < p.H) ? p.w1[(int64_t)i * p.din + k0 + e] * Sw : 0.f;
+      const _Float16 hi = (_Float16)w;
+      v[e] = part ? (_Float16)(w - (float)hi) : hi;
+    }
+    A16[f] = *reinterpret_cast<const uint4*>(&v);
+  }
+  if (DIST) {
+    for (int f = tid; f < C::ADIST; f += THREADS) {
+      const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
+      Adist[f] = (i < p.H) ? p.w1[(int64_t)i * p.din + D + (ln >> 5)] * Sw : 0.f;
+    }
+  }
+  for (int f = tid; f < C::EPI; f += THREADS) {
+    const int which = f / (2 * HB * 16), rem = f % (2 * HB * 16);
+    const int hh2 = rem / (HB * 16), hr = rem % (HB * 16), hb = hr / 16, r = hr % 16;
+    const int i = acc_row(hb, r, hh2);
+    Eimg[f] = (i < p.H) ? (which == 0 ? p.b1[i] : p.w2[i]) : 0.f;
+  }
+
+  // ---- candidate operand t_c (fp32, this lane half's DH dims) and its max magnitude
+  float tv[DH];
+  {
+    const float* src = (REGION && hh) ? p.er + region_of[cc] * p.region_dim
+                                      : p.et + cc * p.item_dim + (REGION ? 0 : hh * DH);
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      tv[4 * q] = v.x;
+      tv[4 * q + 1] = v.y;
+      tv[4 * q + 2] = v.z;
+      tv[4 * q + 3] = v.w;
+    }
+  }
+  float tmax = 0.f;
+#pragma unroll
+  for (int k = 0; k < DH; ++k) tmax = fmaxf(tmax, fabsf(tv[k]));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  double clat = 0.0, clon = 0.0;
+  DistW dw{0.f, 0.f, 0.f};
+  const double* llrow = nullptr;
+  if (DIST) {
+    if (coords) {
+      clat = coords[2 * cc];
+      clon = coords[2 * cc + 1];
+    } else {
+      llrow = latlon_mat + cc * p.P * 2;
+    }
+    dw = load_distw(p, hh);
+  }
+
+  float S = 0.f, N = 0.f;
+  bool in_hist = false;
+  float St = 1.f;                      // current scale applied to tv[]
+  Epi16<HB, EREGS> epi;
+
+  for (int64_t j0 = 0; j0 < hlen; j0 += JC) {
+    const int jn = (int)std::min<int64_t>(JC, hlen - j0);
+    __syncthreads();
+    float hmax = 0.f;
+    for (int f = tid; f < jn * (D / 4); f += THREADS) {
+      const int jj = f / (D / 4), q4 = f % (D / 4);
+      const int64_t item = indices[hbeg + j0 + jj];
+      float4 v;
+      if (!REGION || q4 < DH / 4)
+        v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
+      else
+        v = reinterpret_cast<const float4*>(p.er + region_of[item] * p.region_dim)[q4 - DH / 4];
+      reinterpret_cast<float4*>(hrows)[f] = v;
+      hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int jj = tid; jj < jn; jj += THREADS) {
+      const int64_t item = indices[hbeg + j0 + jj];
+      hid[jj] = (int32_t)item;
+      if (DIST && coords) {
+        hco[2 * jj] = coords[2 * item];
+        hco[2 * jj + 1] = coords[2 * item + 1];
+      }
+    }
+    const float mh = block_max(hmax, red);   // contains the barrier that publishes the chunk
+    const float Snew = pow2_scale(tmax * mh);
+    const float ratio = Snew / St;           // exact: both powers of two
+#pragma unroll
+    for (int k = 0; k < DH; ++k) tv[k] *= ratio;
+    St = Snew;
+    const float invS = 1.f / (Sw * St);
+    epi.rescale(Eimg, hh, Sw * St, invS);
+    const float invSt = 1.f / St;
+
+    for (int jj = 0; jj < jn; ++jj) {
+      const float* hr = hrows + jj * D + hh * DH;
+      floatx16 acc[HB];
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[hb][r] = epi.init(hb * 16 + r);
+      float sd = 0.f;
+      uint4 an[HB][2];
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb) {
+        an[hb][0] = A16[((hb * KS) * 2 + 0) * 64 + lane];
+        an[hb][1] = A16[((hb * KS) * 2 + 1) * 64 + lane];
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        uint4 ac[HB][2];
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) {
+          ac[hb][0] = an[hb][0];
+          ac[hb][1] = an[hb][1];
+        }
+        if (s + 1 < KS) {
+#pragma unroll
+          for (int hb = 0; hb < HB; ++hb) {
+            an[hb][0] = A16[((hb * KS + s + 1) * 2 + 0) * 64 + lane];
+            an[hb][1] = A16[((hb * KS + s + 1) * 2 + 1) * 64 + lane];
+          }
+        }
+        const float4 h0 = *reinterpret_cast<const float4*>(hr + 8 * s);
+        const float4 h1 = *reinterpret_cast<const float4*>(hr + 8 * s + 4);
+        float x[8];
+        x[0] = tv[8 * s + 0] * h0.x;
+        x[1] = tv[8 * s + 1] * h0.y;
+        x[2] = tv[8 * s + 2] * h0.z;
+        x[3] = tv[8 * s + 3] * h0.w;
+        x[4] = tv[8 * s + 4] * h1.x;
+        x[5] = tv[8 * s + 5] * h1.y;
+        x[6] = tv[8 * s + 6] * h1.z;
+        x[7] = tv[8 * s + 7] * h1.w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sd += x[e];
+        half8 xh, xl;
+        split8(x, xh, xl);
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) {
+          const half8 ah = *reinterpret_cast<const half8*>(&ac[hb][0]);
+          const half8 al = *reinterpret_cast<const half8*>(&ac[hb][1]);
+          acc[hb] = mfma16(al, xh, acc[hb]);
+          acc[hb] = mfma16(ah, xl, acc[hb]);
+          acc[hb] = mfma16(ah, xh, acc[hb]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (DIST) {
+        float ll0, ll1;
+        if (coords) {
+          ll0 = (float)fabs(clat - hco[2 * jj]);
+          ll1 = (float)fabs(clon - hco[2 * jj + 1]);
+        } else {
+          ll0 = (float)llrow[2 * (int64_t)hid[jj]];
+          ll1 = (float)llrow[2 * (int64_t)hid[jj] + 1];
+        }
+        const float fs = dist_feature(dw, ll0, ll1) * St;   // exact power-of-two scaling
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) acc[hb] = mfma32(Adist[hb * 64 + lane], fs, acc[hb]);
+      }
+      float ap = 0.f;
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ap += epi.term(hb * 16 + r, acc[hb][r], invS);
+      const float a = ap + __shfl_xor(ap, 32);
+      const float sv = (sd + __shfl_xor(sd, 32)) * invSt;
+      const bool keep = hid[jj] != (int32_t)c;
+      const float e = expf(a) * (keep ? 1.f : 0.f);
+      in_hist |= !keep;
+      S += e;
+      N += e * sv;
+    }
+  }
+
+  const float logit = finish_logit(S, N, p.beta, hlen == 0);
+  const bool isnan_ = logit != logit;
+  float sc = sigmoidf_ref(logit);
+  if (isnan_) sc = __builtin_nanf("");
+  if (in_hist) sc = -1.f;
+  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (nan_count) {
+    const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
+    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-fp16 catalog scorer, item-side factorisation ("x3b"):
+//   W1 (h_j (.) t_c) = (W1 diag(h_j)) t_c = A_j t_c
+// A_j (H x D) is formed ONCE per history item per workgroup, in fp32 (a_ik = w_ik * h_jk), then
+// scaled by S_A and split into fp16 hi/lo in MFMA-A fragment order in an LDS ring (all 512
+// threads build it, one barrier per group of items); t_c is scaled by S_t and split ONCE per
+// candidate into B fragments that stay in VGPRs for the whole sweep. The per-(c, j) VALU work
+// is then only the epilogue and h_j . t_c -- no per-pair conversions.
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB, bool DIST>
+struct CfgB {
+  static constexpr int D = 2 * DH;
+  static constexpr int KS = DH / 8;
+  static constexpr int NE = HB * KS * 64;             // uint4 fragment entries per item (hi or lo)
+  static constexpr int IB = NE * 16 * 2;              // bytes per item (hi + lo)
+#ifdef NAIS_X3B_G
+  static constexpr int G = NAIS_X3B_G;
+#else
+  static constexpr int G = IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1);   // items per ring group
+#endif
+  static constexpr int JCB = (2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;  // LDS chunk rows
+  static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread
+  static constexpr int ADIST = DIST ? HB * 64 : 0;
+  static constexpr int EPI = 2 * 2 * HB * 16;
+  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
+                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+};
+
+template <int DH, int HB, int VAR>
+__global__ void __launch_bounds__(THREADS, 1)
+catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
+                         const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                         const int64_t* __restrict__ region_of, const double* __restrict__ coords,
+                         const double* __restrict__ latlon_mat, float* __restrict__ scores,
+                         int64_t score_ld, int32_t* __restrict__ nan_count) {
+  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  using C = CfgB<DH, HB, DIST>;
+  constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
+  constexpr bool EREGS = HB <= 2 && DH <= 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][hi|lo][NE]
+  float* Adist = reinterpret_cast<float*>(ring + 2 * G * 2 * NE);
+  float* Eimg = Adist + C::ADIST;
+  float* red = Eimg + C::EPI;
+  float* hrows = red + 16;
+  int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
+  double* hco = reinterpret_cast<double*>(hid + JCB);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int64_t u = users[blockIdx.y];
+  const int64_t hbeg = indptr[u];
+  const int64_t hlen = indptr[u + 1] - hbeg;
+  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P;
+  const int64_t cc = valid ? c : p.P - 1;
+
+  // ---- this thread's W1 values for the fragment entries it builds (fp32, unscaled)
+  float wv[EPT][8];
+  float wmax = 0.f;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * THREADS;
+    const int ln = e & 63, s = (e >> 6) % KS, hb = (e >> 6) / KS;
+    const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 8 * s;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      wv[q][x] = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
+      wmax = fmaxf(wmax, fabsf(wv[q][x]));
+    }
+  }
+  const float Wmax = block_max(wmax, red);
+  if (DIST) {
+    for (int f = tid; f < C::ADIST; f += THREADS) {
+      const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
+      Adist[f] = (i < p.H) ? p.w1[(int64_t)i * p.din + D + (ln >> 5)] : 0.f;
+    }
+  }
+  for (int f = tid; f < C::EPI; f += THREADS) {
+    const int which = f / (2 * HB * 16), rem = f % (2 * HB * 16);
+    const int hh2 = rem / (HB * 16), hr = rem % (HB * 16), hb = hr / 16, r = hr % 16;
+    const int i = acc_row(hb, r, hh2);
+    Eimg[f] = (i < p.H) ? (which == 0 ? p.b1[i] : p.w2[i]) : 0.f;
+  }
+
+  // ---- candidate operand: t_c scaled by S_t (fp32 copy for h . t) and its fp16 hi/lo B fragments
+  float tv[DH];
+  {
+    const float* src = (REGION && hh) ? p.er + region_of[cc] * p.region_dim
+                                      : p.et + cc * p.item_dim + (REGION ? 0 : hh * DH);
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(src)[q];
+      tv[4 * q] = v.x;
+      tv[4 * q + 1] = v.y;
+      tv[4 * q + 2] = v.z;
+      tv[4 * q + 3] = v.w;
+    }
+  }
+  float tmax = 0.f;
+#pragma unroll
+  for (int k = 0; k < DH; ++k) tmax = fmaxf(tmax, fabsf(tv[k]));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  const float St = pow2_scale(tmax);
+  const float invSt = 1.f / St;
+  half8 tb_hi[KS], tb_lo[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      tv[8 * s + e] *= St;
+      x[e] = tv[8 * s + e];
+    }
+    split8(x, tb_hi[s], tb_lo[s]);
+  }
+  double clat = 0.0, clon = 0.0;
+  DistW dw{0.f, 0.f, 0.f};
+  const double* llrow = nullptr;
+  if (DIST) {
+    if (coords) {
+      clat = coords[2 * cc];
+      clon = coords[2 * cc + 1];
+    } else {
+      llrow = latlon_mat + cc * p.P * 2;
+    }
+    dw = load_distw(p, hh);
+  }
+
+  float S = 0.f, N = 0.f;
+  bool in_hist = false;
+  Epi16<HB, EREGS> epi;
+
+  // build the fragments of chunk-local item jj into ring slot (grp, it)
+  // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
+  auto build = [&](int jj, int grp, int it) {
+    const float* hr = hrows + jj * D;
+    uint4* dst = ring + ((grp * G + it) * 2) * NE;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * THREADS;
+      if (e < NE) {
+        const int ln = e & 63, s = (e >> 6) % KS;
+        const int k0 = (ln >> 5) * DH + 8 * s;
+        const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
+        const float4 h1 = *reinterpret_cast<const float4*>(hr + k0 + 4);
+        float a[8];
+        a[0] = wv[q][0] * h0.x;
+        a[1] = wv[q][1] * h0.y;
+        a[2] = wv[q][2] * h0.z;
+        a[3] = wv[q][3] * h0.w;
+        a[4] = wv[q][4] * h1.x;
+        a[5] = wv[q][5] * h1.y;
+        a[6] = wv[q][6] * h1.z;
+        a[7] = wv[q][7] * h1.w;
+        half8 hi, lo;
+        split8(a, hi, lo);
+        dst[e] = *reinterpret_cast<const uint4*>(&hi);
+        dst[NE + e] = *reinterpret_cast<const uint4*>(&lo);
+      }
+    }
+  };
+
+  float Sacc = 1.f, invS = 1.f;
+
+  // One pipeline step: the MFMA chain of item `cur` (A_j from the ring slot `src`, t_c from VGPRs)
+  // into accN, with the VALU epilogue of the previous item (accP, chunk-local `prev`) cut into KS
+  // slices placed between the K-steps, so the matrix pipe and the VALU work side by side inside
+  // one wave (A/B: profiles/r1/ab_*.json). `live` = false makes the epilogue a no-op (its result
+  // is selected away), keeping the control flow uniform inside the step.
+  auto step = [&](auto do_mma, const uint4* src, floatx16 (&accN)[HB], const floatx16 (&accP)[HB],
+                  int cur, int prev, bool live) {
+    constexpr bool MMA = decltype(do_mma)::value;
+    constexpr int NV = HB * 16;                 // accumulator values per lane
+    constexpr int VPS = (NV + KS - 1) / KS;     // epilogue values per K-step slice
+    constexpr int QPS = (DH / 4 + KS - 1) / KS; // h . t float4 groups per slice
+    const int pj = live ? prev : 0;
+    const float* hr = hrows + pj * D + hh * DH;
+    float sd = 0.f, ap = 0.f;
+    if (MMA) {
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accN[hb][r] = epi.init(hb * 16 + r);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (MMA) {
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) {
+          const uint4 ahu = src[(hb * KS + s) * 64 + lane];
+          const uint4 alu = src[NE + (hb * KS + s) * 64 + lane];
+          const half8 ah = *reinterpret_cast<const half8*>(&ahu);
+          const half8 al = *reinterpret_cast<const half8*>(&alu);
+          accN[hb] = mfma16(al, tb_hi[s], accN[hb]);
+          accN[hb] = mfma16(ah, tb_lo[s], accN[hb]);
+          accN[hb] = mfma16(ah, tb_hi[s], accN[hb]);
+        }
+      }
+#pragma unroll
+      for (int v = s * VPS; v < (s + 1) * VPS && v < NV; ++v)
+        ap += epi.term(v, accP[v / 16][v % 16], invS);
+#pragma unroll
+      for (int q = s * QPS; q < (s + 1) * QPS && q < DH / 4; ++q) {
+        const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * q);
+        sd = __builtin_fmaf(tv[4 * q], hv.x, sd);
+        sd = __builtin_fmaf(tv[4 * q + 1], hv.y, sd);
+        sd = __builtin_fmaf(tv[4 * q + 2], hv.z, sd);
+        sd = __builtin_fmaf(tv[4 * q + 3], hv.w, sd);
+      }
+      if (NAIS_X3B_SCHED) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (DIST && MMA) {   // the 2 distance columns of item `cur`: exact fp32 MFMA K-step
+      float ll0, ll1;
+      if (coords) {
+        ll0 = (float)fabs(clat - hco[2 * cur]);
+        ll1 = (float)fabs(clon - hco[2 * cur + 1]);
+      } else {
+        ll0 = (float)llrow[2 * (int64_t)hid[cur]];
+        ll1 = (float)llrow[2 * (int64_t)hid[cur] + 1];
+      }
+      const float fs = dist_feature(dw, ll0, ll1) * Sacc;   // exact power-of-two scaling
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb) accN[hb] = mfma32(Adist[hb * 64 + lane], fs, accN[hb]);
+    }
+    const float a = ap + __shfl_xor(ap, 32);
+    const float sv = (sd + __shfl_xor(sd, 32)) * invSt;
+    const bool keep = hid[pj] != (int32_t)c;
+    const float e = expf(a) * (keep ? 1.f : 0.f);
+    if (live) {
+      in_hist |= !keep;
+      S += e;
+      N += e * sv;
+    }
+  };
+
+  float SAcur = 1.f;
+  floatx16 accP[HB];
+  for (int64_t j0 = 0; j0 < hlen; j0 += JCB) {
+    const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
+    __syncthreads();
+    float hmax = 0.f;
+    for (int f = tid; f < jn * (D / 4); f += THREADS) {
+      const int jj = f / (D / 4), q4 = f % (D / 4);
+      const int64_t item = indices[hbeg + j0 + jj];
+      float4 v;
+      if (!REGION || q4 < DH / 4)
+        v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
+      else
+        v = reinterpret_cast<const float4*>(p.er + region_of[item] * p.region_dim)[q4 - DH / 4];
+      reinterpret_cast<float4*>(hrows)[f] = v;
+      hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int jj = tid; jj < jn; jj += THREADS) {
+      const int64_t item = indices[hbeg + j0 + jj];
+      hid[jj] = (int32_t)item;
+      if (DIST && coords) {
+        hco[2 * jj] = coords[2 * item];
+        hco[2 * jj + 1] = coords[2 * item + 1];
+      }
+    }
+    const float SA = pow2_scale(Wmax * block_max(hmax, red));   // barrier: chunk published
+    const float rs = SA / SAcur;                                  // exact power-of-two ratio
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) wv[q][x] *= rs;
+    SAcur = SA;
+    Sacc = SA * St;
+    invS = 1.f / Sacc;
+    epi.rescale(Eimg, hh, Sacc, invS);
+    const int ngroups = (jn + G - 1) / G;
+#pragma unroll
+    for (int it = 0; it < G; ++it)
+      if (it < jn) build(it, 0, it);
+    __syncthreads();
+    int prev = -1;                      // chunk-local item whose epilogue is pending in accP
+    for (int g = 0; g < ngroups; ++g) {
+      if (g + 1 < ngroups) {
+#pragma unroll
+        for (int it = 0; it < G; ++it) {
+          const int jj = (g + 1) * G + it;
+          if (jj < jn) build(jj, (g + 1) & 1, it);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < G; ++it) {
+        const int jj = g * G + it;
+        if (jj < jn) {
+          floatx16 accN[HB];
+          step(std::true_type{}, ring + (((g & 1) * G + it) * 2) * NE, accN, accP, jj, prev,
+               prev >= 0);
+#pragma unroll
+          for (int hb = 0; hb < HB; ++hb) accP[hb] = accN[hb];
+          prev = jj;
+        }
+      }
+      __syncthreads();
+    }
+    if (prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
+      floatx16 accN[HB];
+      step(std::false_type{}, ring, accN, accP, 0, prev, true);
+    }
+  }
+
+  const float logit = finish_logit(S, N, p.beta, hlen == 0);
+  const bool isnan_ = logit != logit;
+  float sc = sigmoidf_ref(logit);
+  if (isnan_) sc = __builtin_nanf("");
+  if (in_hist) sc = -1.f;
+  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (nan_count) {
+    const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
+    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Top-k per user (validation.py:26-27): exact radix select on 64-bit keys
 //   key = ordered(score) << 32 | (0xFFFFFFFF - poi)   -> unique; larger key = (higher score, lower id)
 // 8 MSB-first 8-bit passes over the user's score row (L2-resident), then the k winners are
@@ -600,6 +1264,9 @@ struct Shape {
 int validate(const nais_params_t* p, Shape* sh) {
   if (!p) return fail(NAIS_E_INVALID, "params is NULL");
   if (p->variant < 0 || p->variant > 2) return fail(NAIS_E_INVALID, "unknown variant");
+  if (p->precision != NAIS_PRECISION_FP32 && p->precision != NAIS_PRECISION_FP16X3 &&
+      p->precision != NAIS_PRECISION_FP16X3_PAIRSPLIT)
+    return fail(NAIS_E_INVALID, "unknown precision");
   if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
     return fail(NAIS_E_INVALID, "missing parameter pointer");
   if (p->num_pois <= 0) return fail(NAIS_E_INVALID, "num_pois must be > 0");
@@ -669,6 +1336,65 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
   hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
                      coords, latlon_mat, scores, ld, nan_count);
   return check_launch("catalog_score_kernel");
+}
+
+template <int DH, int HB, int VAR>
+size_t catalog_x3_lds() {
+  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  return Consts16<DH, HB, DIST>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
+         (DIST ? size_t(JC) * 16 : 0);
+}
+
+template <int DH, int HB, int VAR>
+int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* indices,
+                      const int32_t* users, int nb, const int64_t* region_of, const double* coords,
+                      const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
+                      hipStream_t stream) {
+  if constexpr (DH % 8 != 0) {  // D = 8: one K=16 f16 step would be half padding; use fp32
+    return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
+                                       scores, ld, nan_count, stream);
+  } else {
+    const size_t lds = catalog_x3_lds<DH, HB, VAR>();
+    auto kern = catalog_score_x3_kernel<DH, HB, VAR>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+    hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
+                       coords, latlon_mat, scores, ld, nan_count);
+    return check_launch("catalog_score_x3_kernel");
+  }
+}
+
+template <int DH, int HB, int VAR>
+int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
+                       const int32_t* users, int nb, const int64_t* region_of, const double* coords,
+                       const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
+                       hipStream_t stream) {
+  if constexpr (DH % 8 != 0) {
+    return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
+                                       scores, ld, nan_count, stream);
+  } else if constexpr (!(HB <= 2 && DH <= 32 && VAR != NAIS_VARIANT_REGION_DISTANCE)) {
+    // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel
+    return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
+                                          latlon_mat, scores, ld, nan_count, stream);
+  } else {
+    const size_t lds = CfgB<DH, HB, VAR == NAIS_VARIANT_REGION_DISTANCE>::BYTES;
+    auto kern = catalog_score_x3b_kernel<DH, HB, VAR>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+    dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+    hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
+                       coords, latlon_mat, scores, ld, nan_count);
+    return check_launch("catalog_score_x3b_kernel");
+  }
 }
 
 template <int DH, int HB, int VAR>
@@ -787,8 +1513,15 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
   const int64_t ld = round_up(params->num_pois, 64);
   for (int32_t u0 = 0; u0 < num_users; u0 += MAX_BATCH_USERS) {
     const int nb = std::min<int32_t>(MAX_BATCH_USERS, num_users - u0);
-    NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
-                  region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    if (params->precision == NAIS_PRECISION_FP16X3)
+      NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X3_PAIRSPLIT)
+      NAIS_DISPATCH(launch_catalog_x3, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    else
+      NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
+                    region_of, coords, latlon_mat, scores, ld, nan_count, st);
     if (rc) return rc;
     hipLaunchKernelGGL(topk_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld,
                        params->num_pois, k, out_ids + (int64_t)u0 * k,
@@ -821,9 +1554,18 @@ int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,
   if (rc) return rc;
   for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
     const int nb = std::min<int32_t>(65535, num_users - u0);
-    NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
-                  region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
-                  nan_count, st);
+    if (params->precision == NAIS_PRECISION_FP16X3)
+      NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                    nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X3_PAIRSPLIT)
+      NAIS_DISPATCH(launch_catalog_x3, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                    nan_count, st);
+    else
+      NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
+                    region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                    nan_count, st);
     if (rc) return rc;
   }
   return NAIS_OK;

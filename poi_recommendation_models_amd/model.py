@@ -27,6 +27,13 @@ class _NAISDevice(nn.Module):
 
     VARIANT = _capi.VARIANT_BASIC
     report_nan = True  # model.py:50-54 prints the NaN count of every forward
+    # arithmetic of the catalog scorer's W1 x products (include/nais.h NAIS_PRECISION_*):
+    #   "fp16x3" (default) split-fp16 MFMA, 3 products per fp32 product, fp32 accumulation,
+    #            ~2^-21 relative per product -- 2.6x the fp32 path, same max |dscore| vs the
+    #            reference on every golden set (tests/test_gpu_parity.py);
+    #   "fp32"   exact fp32 MFMA (a k-ordered fmaf chain); "fp16x3_pairsplit" alternative split.
+    # nais_forward (the general model.forward path) is always fp32.
+    precision = "fp16x3"
 
     def _check_device(self, *tensors):
         dev = self.embed_history.weight.device
@@ -53,6 +60,8 @@ class _NAISDevice(nn.Module):
         p.num_pois = self.embed_history.weight.shape[0]
         p.num_regions = self.embed_region.weight.shape[0] if hasattr(self, "embed_region") else 0
         p.beta = float(self.beta)
+        p.precision = {"fp32": _capi.PRECISION_FP32, "fp16x3": _capi.PRECISION_FP16X3,
+                       "fp16x3_pairsplit": _capi.PRECISION_FP16X3_PAIRSPLIT}[self.precision]
         p.embed_history = self.embed_history.weight.data_ptr()
         p.embed_target = self.embed_target.weight.data_ptr()
         p.embed_region = self.embed_region.weight.data_ptr() if hasattr(self, "embed_region") else None
