@@ -61,6 +61,22 @@ struct DevParams {
   float beta;
 };
 
+#ifndef NAIS_TILE_MAJOR
+#define NAIS_TILE_MAJOR 0
+#endif
+// Catalog grid: one workgroup per (user slot, 256-POI tile). Default user-major dispatch order
+// (blockIdx.x = tile): a user's ~400 workgroups run back to back, heaviest users first.
+// NAIS_TILE_MAJOR=1 swaps the order so that workgroups reading the same 64 KB of target rows
+// share an XCD's L2 (fabric traffic 6.7 GB -> ~0.2 GB per 256-user launch) -- measured slower
+// (fp32 -11 %, fp16x3 -3 %, profiles/r1/ab_tilemajor.json): the kernel is MFMA-bound and the
+// Infinity Cache serves the re-reads at ~40 GB/s, far below any limit.
+__device__ __forceinline__ int cat_user_slot() { return NAIS_TILE_MAJOR ? blockIdx.x : blockIdx.y; }
+__device__ __forceinline__ int cat_tile() { return NAIS_TILE_MAJOR ? blockIdx.y : blockIdx.x; }
+inline dim3 cat_grid(int64_t P, int nb, int cand_per_block) {
+  const unsigned tiles = (unsigned)((P + cand_per_block - 1) / cand_per_block);
+  return NAIS_TILE_MAJOR ? dim3((unsigned)nb, tiles) : dim3(tiles, (unsigned)nb);
+}
+
 __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -247,10 +263,10 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JC);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[blockIdx.y];
+  const int64_t u = users[cat_user_slot()];
   const int64_t hbeg = indptr[u];
   const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
   const bool valid = c < p.P;
   const int64_t cc = valid ? c : p.P - 1;
 
@@ -333,7 +349,7 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float sc = sigmoidf_ref(logit);
   if (isnan_) sc = __builtin_nanf("");
   if (in_hist) sc = -1.f;  // history POI: not a candidate (batches.py:56)
-  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (valid && hh == 0) scores[(int64_t)cat_user_slot() * score_ld + c] = sc;
   if (nan_count) {
     const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
     if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
@@ -570,10 +586,10 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JC);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[blockIdx.y];
+  const int64_t u = users[cat_user_slot()];
   const int64_t hbeg = indptr[u];
   const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
   const bool valid = c < p.P;
   const int64_t cc = valid ? c : p.P - 1;
 
@@ -765,7 +781,7 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float sc = sigmoidf_ref(logit);
   if (isnan_) sc = __builtin_nanf("");
   if (in_hist) sc = -1.f;
-  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (valid && hh == 0) scores[(int64_t)cat_user_slot() * score_ld + c] = sc;
   if (nan_count) {
     const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
     if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
@@ -822,10 +838,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JCB);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[blockIdx.y];
+  const int64_t u = users[cat_user_slot()];
   const int64_t hbeg = indptr[u];
   const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)blockIdx.x * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
   const bool valid = c < p.P;
   const int64_t cc = valid ? c : p.P - 1;
 
@@ -1082,7 +1098,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float sc = sigmoidf_ref(logit);
   if (isnan_) sc = __builtin_nanf("");
   if (in_hist) sc = -1.f;
-  if (valid && hh == 0) scores[(int64_t)blockIdx.y * score_ld + c] = sc;
+  if (valid && hh == 0) scores[(int64_t)cat_user_slot() * score_ld + c] = sc;
   if (nan_count) {
     const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
     if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
@@ -1270,6 +1286,7 @@ int validate(const nais_params_t* p, Shape* sh) {
   if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
     return fail(NAIS_E_INVALID, "missing parameter pointer");
   if (p->num_pois <= 0) return fail(NAIS_E_INVALID, "num_pois must be > 0");
+  if (p->num_pois > 65535ll * 256) return fail(NAIS_E_UNSUPPORTED, "num_pois > 16.7M (grid.y limit)");
   const int D = p->embed_dim;
   if (D <= 0 || D % 8 != 0 || D > 128)
     return fail(NAIS_E_UNSUPPORTED, "embed_dim must be a multiple of 8 in [8, 128]");
@@ -1332,7 +1349,7 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+  dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
   hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
                      coords, latlon_mat, scores, ld, nan_count);
   return check_launch("catalog_score_kernel");
@@ -1362,7 +1379,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+    dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
                        coords, latlon_mat, scores, ld, nan_count);
     return check_launch("catalog_score_x3_kernel");
@@ -1390,7 +1407,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid((unsigned)((d.P + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)nb);
+    dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
                        coords, latlon_mat, scores, ld, nan_count);
     return check_launch("catalog_score_x3b_kernel");
