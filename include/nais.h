@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 2
+#define NAIS_ABI_VERSION 3
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -81,9 +81,10 @@ typedef struct nais_params {
   const float* dist_b;          /* dist_layer.bias      [2]    | NULL                                 */
 } nais_params_t;
 
-/* Optional power-law geo prior blended into the catalog scores (powerLaw.py:86-92, run.py:55-59,
- * run.py:537-539): score' = (1-alpha)*score + alpha * G(u,c)/max_c G(u,c), G = prod_j a*max(0.01,dist)^b.
- * Not yet implemented in ABI v1: pass NULL. */
+/* Optional power-law geo prior blended into the catalog scores before the top-k (powerLaw.py:86-92,
+ * run.py:55-59, run.py:537-539): G(u,c) = prod_j a*max(0.01, dist(coo_j, coo_c))^b (float64, history in
+ * CSR order), G_norm = G / max_c G (unless the max is 0), score' = f32((1-alpha)*score) + alpha*G_norm
+ * (float64), ranked on score'. out_scores then carries score' rounded to float32. */
 typedef struct nais_prior {
   double a, b, alpha;
   const double* coords;         /* [P, 2] (lat, lng) float64 */
@@ -129,7 +130,8 @@ int32_t nais_forward(const nais_params_t* params,
  *   caller checks -- the kernel writes id -1 / NaN for missing slots and counts them in *short_count).
  *   nan_count / short_count (device int32, may be NULL) are atomically incremented.
  */
-size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k);
+size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k,
+                                      int32_t with_prior);
 int32_t nais_score_topk(const nais_params_t* params,
                         const int64_t* indptr, const int64_t* indices,
                         const int32_t* users, int32_t num_users, int32_t k,
@@ -150,6 +152,24 @@ int32_t nais_score_catalog(const nais_params_t* params,
                            const int32_t* users, int32_t num_users,
                            const int64_t* region_of, const double* coords, const double* latlon_mat,
                            float* scores, int64_t score_ld, int32_t* nan_count, void* stream);
+
+/*
+ * Power-law prior rows (powerLaw.py:90-92): out[i * out_ld + c] = prod_j pr_d(dist(coo_j, coo_c)) for user
+ * users[i], c in [0, P), float64 in the reference's operation order; history POIs get -1. out_max[i] =
+ * max over the user's candidates (the normalize() divisor of run.py:55-59). coords [P, 2] float64.
+ */
+int32_t nais_powerlaw_prior(const double* coords, int64_t num_pois, const int64_t* indptr,
+                            const int64_t* indices, const int32_t* users, int32_t num_users, double a,
+                            double b, double* out, int64_t out_ld, double* out_max, void* stream);
+
+/*
+ * Pair-distance histogram for PowerLaw.fit_distance_distribution (powerLaw.py:41-55): hist[bin] = number of
+ * pairs i < j within a user's history (all num_users users) with int(dist) == bin (km); pairs with
+ * dist >= nbins or NaN are counted in *overflow. Both outputs are zeroed by the call.
+ */
+int32_t nais_distance_histogram(const double* coords, const int64_t* indptr, const int64_t* indices,
+                                int64_t num_users, uint64_t* hist, int64_t nbins, uint64_t* overflow,
+                                void* stream);
 
 /*
  * Top-k of score rows (the second half of nais_score_topk): for row i in [0, num_rows), the k largest

@@ -12,13 +12,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE = 0, 1, 2
 FLAG_SIGMOID = 1
 
 EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_topk_workspace_size",
-           "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_gather_rows")
+           "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_powerlaw_prior",
+           "nais_distance_histogram", "nais_gather_rows")
 
 
 class NaisParams(ctypes.Structure):
@@ -32,6 +33,12 @@ class NaisParams(ctypes.Structure):
         ("embed_region", ctypes.c_void_p), ("w1", ctypes.c_void_p), ("b1", ctypes.c_void_p),
         ("w2", ctypes.c_void_p), ("dist_w", ctypes.c_void_p), ("dist_b", ctypes.c_void_p),
     ]
+
+
+class NaisPrior(ctypes.Structure):
+    """Mirror of `nais_prior_t`."""
+    _fields_ = [("a", ctypes.c_double), ("b", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("coords", ctypes.c_void_p)]
 
 
 class NaisError(RuntimeError):
@@ -63,15 +70,20 @@ def load(path: str | None = None):
     lib.nais_forward.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, i64, vp, vp,
                                  i64, vp, vp, i32, vp]
     lib.nais_score_topk_workspace_size.restype = sz
-    lib.nais_score_topk_workspace_size.argtypes = [ctypes.POINTER(NaisParams), i32, i32]
+    lib.nais_score_topk_workspace_size.argtypes = [ctypes.POINTER(NaisParams), i32, i32, i32]
     lib.nais_score_topk.restype = i32
     lib.nais_score_topk.argtypes = [ctypes.POINTER(NaisParams), vp, vp, vp, i32, i32, vp, vp, vp,
-                                    vp, vp, vp, vp, vp, vp, sz, vp]
+                                    ctypes.c_void_p, vp, vp, vp, vp, vp, sz, vp]
     lib.nais_score_catalog.restype = i32
     lib.nais_score_catalog.argtypes = [ctypes.POINTER(NaisParams), vp, vp, vp, i32, vp, vp, vp, vp,
                                        i64, vp, vp]
     lib.nais_topk_rows.restype = i32
     lib.nais_topk_rows.argtypes = [vp, i64, i64, i32, i32, vp, vp, vp, vp]
+    f64 = ctypes.c_double
+    lib.nais_powerlaw_prior.restype = i32
+    lib.nais_powerlaw_prior.argtypes = [vp, i64, vp, vp, vp, i32, f64, f64, vp, i64, vp, vp]
+    lib.nais_distance_histogram.restype = i32
+    lib.nais_distance_histogram.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp]
     lib.nais_gather_rows.restype = i32
     lib.nais_gather_rows.argtypes = [vp, i64, i32, vp, i64, vp, vp]
     v = lib.nais_abi_version()

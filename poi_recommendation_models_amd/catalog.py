@@ -10,6 +10,8 @@ per user. Nothing per-candidate crosses PCIe.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -107,10 +109,13 @@ def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlo
 
 
 def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlon_mat=None,
-               ordered=True, stream=None):
+               ordered=True, stream=None, prior=None):
     """Top-k (ids int64 [len(users), k], scores f32) of every listed user over its complement
     candidates, ordered (score desc, POI id asc). Raises like torch.topk when a user has fewer
-    than k candidates (validation.py:26)."""
+    than k candidates (validation.py:26).
+
+    `prior` = (a, b, alpha, poi_coords): rank on the power-law-blended score
+    f32((1-alpha) * score) + alpha * G / max G instead (run.py:537-539, powerLaw.py:86-92)."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model.embed_history.weight.shape[0]
@@ -131,11 +136,17 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
     lib = _capi.load()
     prm = model.nais_params()
-    nbytes = lib.nais_score_topk_workspace_size(prm, n, k)
+    pri, pri_coords = None, None
+    if prior is not None:
+        pa, pb, alpha, pc = prior
+        pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
+        pri = _capi.NaisPrior(float(pa), float(pb), float(alpha), pri_coords.data_ptr())
+    nbytes = lib.nais_score_topk_workspace_size(prm, n, k, int(prior is not None))
     ws = _workspace(dev, nbytes)
     st = stream if stream is not None else _capi.stream_handle(dev)
     rc = lib.nais_score_topk(prm, csr.indptr.data_ptr(), csr.indices.data_ptr(), u_dev.data_ptr(),
-                             n, k, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm), None,
+                             n, k, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
+                             None if pri is None else ctypes.byref(pri),
                              ids.data_ptr(), sc.data_ptr(), counters[0:1].data_ptr(),
                              counters[1:2].data_ptr(), ws.data_ptr(), ws.numel(), st)
     _capi.check(rc, "nais_score_topk")
@@ -147,3 +158,22 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
         inv_t = torch.from_numpy(inv).to(dev)
         ids, sc = ids.index_select(0, inv_t), sc.index_select(0, inv_t)
     return ids.to(torch.int64), sc
+
+
+def prior_rows(train_matrix, users, a, b, coords, device):
+    """Power-law prior rows G [len(users), P] float64 (history POIs = -1) and the per-user max
+    over candidates, via nais_powerlaw_prior (powerLaw.py:90-92, run.py:55-59)."""
+    dev = torch.device(device)
+    csr = device_csr(train_matrix, dev)
+    P = csr.shape[1]
+    users = np.asarray(list(users), dtype=np.int64)
+    u_dev = torch.from_numpy(users.astype(np.int32)).to(dev)
+    cor = torch.as_tensor(np.ascontiguousarray(coords, dtype=np.float64)).to(dev)
+    out = torch.empty(len(users), P, dtype=torch.float64, device=dev)
+    mx = torch.empty(len(users), dtype=torch.float64, device=dev)
+    rc = _capi.load().nais_powerlaw_prior(cor.data_ptr(), P, csr.indptr.data_ptr(),
+                                          csr.indices.data_ptr(), u_dev.data_ptr(), len(users),
+                                          float(a), float(b), out.data_ptr(), P, mx.data_ptr(),
+                                          _capi.stream_handle(dev))
+    _capi.check(rc, "nais_powerlaw_prior")
+    return out, mx

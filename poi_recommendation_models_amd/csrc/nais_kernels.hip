@@ -1232,6 +1232,286 @@ topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k
 }
 
 // ---------------------------------------------------------------------------------------------
+// Power-law geo prior (powerLaw.py:7-21, 86-92) and its blend (run.py:55-59, 537-539).
+// float64 throughout, in the reference's operation order; every product/sum is an explicit
+// round-to-nearest op (__dmul_rn / __dadd_rn / __dsub_rn) so the compiler cannot contract FMAs.
+// Per POI: phi = (90 - lat) * d2r, theta = lng * d2r (d2r = math.pi / 180.0).
+// ---------------------------------------------------------------------------------------------
+constexpr double kD2R = 0.017453292519943295;  // math.pi / 180.0
+
+struct Geo {
+  double lat, lng, sphi, cphi, theta;
+};
+
+__device__ __forceinline__ Geo make_geo(double lat, double lng) {
+  const double phi = __dmul_rn(__dsub_rn(90.0, lat), kD2R);
+  return Geo{lat, lng, sin(phi), cos(phi), __dmul_rn(lng, kD2R)};
+}
+
+// powerLaw.dist(loc1, loc2): loc1 = history POI, loc2 = candidate (powerLaw.py:92)
+__device__ __forceinline__ double ref_dist(const Geo& p1, const Geo& p2) {
+  if (fabs(__dsub_rn(p1.lat, p2.lat)) < 1e-6 && fabs(__dsub_rn(p1.lng, p2.lng)) < 1e-6) return 0.0;
+  const double cosv = __dadd_rn(__dmul_rn(__dmul_rn(p1.sphi, p2.sphi), cos(__dsub_rn(p1.theta, p2.theta))),
+                                __dmul_rn(p1.cphi, p2.cphi));
+  return __dmul_rn(acos(cosv), 6371.0);
+}
+
+// PowerLaw.pr_d (powerLaw.py:86-88): a * max(0.01, d) ** b   (Python max(0.01, nan) = 0.01)
+__device__ __forceinline__ double ref_pr_d(double a, double b, double d) {
+  const double dd = (d > 0.01) ? d : 0.01;
+  return __dmul_rn(a, pow(dd, b));
+}
+
+constexpr int PRIOR_THREADS = 256;
+constexpr int PRIOR_JC = 256;
+
+// G[slot][c] = prod_j pr_d(dist(coo_j, coo_c)) over the user's history in CSR order
+// (np.prod, powerLaw.py:92); history POIs get -1. gmax[slot] = max over candidates (u64 bits).
+__global__ void __launch_bounds__(PRIOR_THREADS)
+prior_kernel(const double* __restrict__ coords, int64_t P, const int64_t* __restrict__ indptr,
+             const int64_t* __restrict__ indices, const int32_t* __restrict__ users, double pa,
+             double pb, double* __restrict__ G, int64_t ld, unsigned long long* __restrict__ gmax) {
+  __shared__ Geo hg[PRIOR_JC];
+  __shared__ int32_t hid[PRIOR_JC];
+  __shared__ double red[PRIOR_THREADS / 64];
+  const int tid = threadIdx.x;
+  const int64_t u = users[blockIdx.y];
+  const int64_t hbeg = indptr[u], hlen = indptr[u + 1] - hbeg;
+  const int64_t c = (int64_t)blockIdx.x * PRIOR_THREADS + tid;
+  const bool valid = c < P;
+  const int64_t cc = valid ? c : P - 1;
+  const Geo gc = make_geo(coords[2 * cc], coords[2 * cc + 1]);
+  double g = 1.0;
+  bool in_hist = false;
+  for (int64_t j0 = 0; j0 < hlen; j0 += PRIOR_JC) {
+    const int jn = (int)std::min<int64_t>(PRIOR_JC, hlen - j0);
+    __syncthreads();
+    for (int jj = tid; jj < jn; jj += PRIOR_THREADS) {
+      const int64_t item = indices[hbeg + j0 + jj];
+      hid[jj] = (int32_t)item;
+      hg[jj] = make_geo(coords[2 * item], coords[2 * item + 1]);
+    }
+    __syncthreads();
+    for (int jj = 0; jj < jn; ++jj) {
+      g = __dmul_rn(g, ref_pr_d(pa, pb, ref_dist(hg[jj], gc)));
+      in_hist |= hid[jj] == (int32_t)c;
+    }
+  }
+  if (hlen == 0) g = 1.0;   // np.prod([]) == 1.0
+  if (valid) G[(int64_t)blockIdx.y * ld + c] = in_hist ? -1.0 : g;
+  double m = (valid && !in_hist) ? g : -1.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    double mm = red[0];
+    for (int w = 1; w < PRIOR_THREADS / 64; ++w) mm = fmax(mm, red[w]);
+    if (mm >= 0.0) atomicMax(gmax + blockIdx.y, (unsigned long long)__double_as_longlong(mm));
+  }
+}
+
+// blended score of candidate c (run.py:537-539 with normalize run.py:55-59):
+//   (1 - alpha) * pred  in float32 (torch: f32 tensor * python scalar), then + alpha * G_norm in f64
+__device__ __forceinline__ bool blended(const float* s, const double* g, double gm, float om_alpha_f,
+                                        double alpha, int64_t c, double& out) {
+  const float v = s[c];
+  if (v < 0.f) return false;                       // history POI: not a candidate
+  const double gn = (gm != 0.0) ? __ddiv_rn(g[c], gm) : g[c];
+  out = __dadd_rn((double)(v * om_alpha_f), __dmul_rn(alpha, gn));
+  return true;
+}
+
+__device__ __forceinline__ unsigned long long ord_f64(double d) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  if (d != d) u = 0x7ff8000000000000ull;           // canonical NaN ranks first (torch.topk)
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double unord_f64(unsigned long long o) {
+  const unsigned long long u = (o & 0x8000000000000000ull) ? (o & 0x7fffffffffffffffull) : ~o;
+  return __longlong_as_double((long long)u);
+}
+
+// top-k over the f64 blended scores: radix select on the 64-bit ordered score (8 passes), then
+// on ~id among the scores equal to the threshold (4 passes), collect, bitonic sort by (score, ~id).
+__global__ void __launch_bounds__(TOPK_THREADS)
+topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const double* __restrict__ G,
+                  int64_t g_ld, const unsigned long long* __restrict__ gmax, int64_t P, int k,
+                  float om_alpha_f, double alpha, int32_t* __restrict__ out_ids,
+                  float* __restrict__ out_scores, int32_t* __restrict__ short_count) {
+  __shared__ uint32_t hist[256];
+  __shared__ unsigned long long bs[MAX_K];
+  __shared__ uint32_t bi[MAX_K];
+  __shared__ uint32_t sh_bin, sh_above, sh_total, sh_cnt;
+  const float* s = scores + (int64_t)blockIdx.x * score_ld;
+  const double* g = G + (int64_t)blockIdx.x * g_ld;
+  const double gm = __longlong_as_double((long long)gmax[blockIdx.x]);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long prefix = 0, mask = 0;       // over the score key
+  uint32_t iprefix = 0, imask = 0;               // over ~id, among score == threshold
+  uint32_t rem = (uint32_t)k;
+  int kk = k;
+  for (int pass = 0; pass < 12; ++pass) {
+    const bool idpass = pass >= 8;
+    const int shift = idpass ? 24 - 8 * (pass - 8) : 56 - 8 * pass;
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
+      double v;
+      if (!blended(s, g, gm, om_alpha_f, alpha, c, v)) continue;
+      const unsigned long long key = ord_f64(v);
+      if (!idpass) {
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+      } else if (key == prefix) {
+        const uint32_t ik = 0xFFFFFFFFu - (uint32_t)c;
+        if ((ik & imask) == iprefix) atomicAdd(&hist[(ik >> shift) & 255], 1u);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int base = 255 - lane * 4;
+      const uint32_t c0 = hist[base], c1 = hist[base - 1], c2 = hist[base - 2], c3 = hist[base - 3];
+      const uint32_t local = c0 + c1 + c2 + c3;
+      uint32_t incl = local;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      if (pass == 0 && lane == 0) sh_total = total;
+      uint32_t need = rem;
+      if (pass == 0 && total < need) need = total;
+      const uint32_t excl = incl - local;
+      if (need > 0 && excl < need && incl >= need) {
+        uint32_t cum = excl;
+        int bsel;
+        if (cum + c0 >= need) bsel = base;
+        else if ((cum += c0) + c1 >= need) bsel = base - 1;
+        else if ((cum += c1) + c2 >= need) bsel = base - 2;
+        else { cum += c2; bsel = base - 3; }
+        sh_bin = (uint32_t)bsel;
+        sh_above = cum;
+      }
+      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; }
+    }
+    __syncthreads();
+    if (pass == 0) {
+      if (sh_total < (uint32_t)kk) kk = (int)sh_total;
+      rem = (uint32_t)kk;
+    }
+    if (!idpass) {
+      prefix |= (unsigned long long)sh_bin << shift;
+      mask |= 255ull << shift;
+    } else {
+      iprefix |= sh_bin << shift;
+      imask |= 255u << shift;
+    }
+    rem -= sh_above;
+    __syncthreads();
+  }
+  if (tid == 0) sh_cnt = 0;
+  __syncthreads();
+  if (kk > 0) {
+    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
+      double v;
+      if (!blended(s, g, gm, om_alpha_f, alpha, c, v)) continue;
+      const unsigned long long key = ord_f64(v);
+      const uint32_t ik = 0xFFFFFFFFu - (uint32_t)c;
+      if (key > prefix || (key == prefix && ik >= iprefix)) {
+        const uint32_t pos = atomicAdd(&sh_cnt, 1u);
+        if (pos < (uint32_t)MAX_K) {
+          bs[pos] = key;
+          bi[pos] = ik;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < k) n2 <<= 1;
+  for (int i = tid; i < n2; i += TOPK_THREADS)
+    if (i >= kk) {
+      bs[i] = 0ull;
+      bi[i] = 0u;
+    }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2; i += TOPK_THREADS) {
+        const int partner = i ^ stride;
+        if (partner > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long x = bs[i], y = bs[partner];
+          const uint32_t xi = bi[i], yi = bi[partner];
+          const bool less = (x < y) || (x == y && xi < yi);
+          const bool greater = (x > y) || (x == y && xi > yi);
+          if (desc ? less : greater) {
+            bs[i] = y;
+            bs[partner] = x;
+            bi[i] = yi;
+            bi[partner] = xi;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += TOPK_THREADS) {
+    int32_t id = -1;
+    float sc = __builtin_nanf("");
+    if (i < kk) {
+      id = (int32_t)(0xFFFFFFFFu - bi[i]);
+      sc = (float)unord_f64(bs[i]);
+    }
+    out_ids[(int64_t)blockIdx.x * k + i] = id;
+    out_scores[(int64_t)blockIdx.x * k + i] = sc;
+  }
+  if (tid == 0 && kk < k && short_count) atomicAdd(short_count, 1);
+}
+
+// Distance histogram for PowerLaw.fit_distance_distribution (powerLaw.py:41-55): every pair
+// i < j of every user's history (CSR order), bin = int(dist(coo_i, coo_j)) (truncation, km).
+constexpr int HIST_LDS_BINS = 4096;
+__global__ void __launch_bounds__(256)
+distance_histogram_kernel(const double* __restrict__ coords, const int64_t* __restrict__ indptr,
+                          const int64_t* __restrict__ indices, int64_t num_users,
+                          unsigned long long* __restrict__ hist, int64_t nbins,
+                          unsigned long long* __restrict__ overflow) {
+  __shared__ uint32_t lh[HIST_LDS_BINS];
+  const int tid = threadIdx.x;
+  const int lb = (int)std::min<int64_t>(nbins, HIST_LDS_BINS);
+  for (int i = tid; i < lb; i += 256) lh[i] = 0;
+  __syncthreads();
+  for (int64_t u = blockIdx.x; u < num_users; u += gridDim.x) {
+    const int64_t b = indptr[u], n = indptr[u + 1] - b;
+    const int64_t npairs = n * (n - 1) / 2;
+    for (int64_t pidx = tid; pidx < npairs; pidx += 256) {
+      // pair index -> (i, j), i < j, row-major over the strict upper triangle
+      int64_t i = (int64_t)((2.0 * n - 1.0 - sqrt((2.0 * n - 1.0) * (2.0 * n - 1.0) - 8.0 * (double)pidx)) / 2.0);
+      if (i < 0) i = 0;
+      while (i > 0 && i * (2 * n - i - 1) / 2 > pidx) --i;
+      while ((i + 1) * (2 * n - i - 2) / 2 <= pidx) ++i;
+      const int64_t j = pidx - i * (2 * n - i - 1) / 2 + i + 1;
+      const int64_t li = indices[b + i], lj = indices[b + j];
+      const Geo gi = make_geo(coords[2 * li], coords[2 * li + 1]);
+      const Geo gj = make_geo(coords[2 * lj], coords[2 * lj + 1]);
+      const double d = ref_dist(gi, gj);
+      if (!(d >= 0.0) || d >= (double)nbins) {   // NaN or beyond the table
+        atomicAdd(overflow, 1ull);
+        continue;
+      }
+      const int64_t bin = (int64_t)d;
+      if (bin < lb) atomicAdd(&lh[bin], 1u);
+      else atomicAdd(hist + bin, 1ull);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < lb; i += 256)
+    if (lh[i]) atomicAdd(hist + i, (unsigned long long)lh[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Standalone row gather (HBM roofline kernel): 16 B per lane, one row per dim/4 lanes.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
@@ -1460,6 +1740,17 @@ int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+int launch_prior(const double* coords, int64_t P, const int64_t* indptr, const int64_t* indices,
+                 const int32_t* users, int nb, double a, double b, double* G, int64_t ld,
+                 unsigned long long* gmax, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(gmax, 0, sizeof(unsigned long long) * nb, st);
+  if (e != hipSuccess) return fail(NAIS_E_HIP, std::string("memset: ") + hipGetErrorString(e));
+  dim3 grid((unsigned)((P + PRIOR_THREADS - 1) / PRIOR_THREADS), (unsigned)nb);
+  hipLaunchKernelGGL(prior_kernel, grid, dim3(PRIOR_THREADS), 0, st, coords, P, indptr, indices,
+                     users, a, b, G, ld, gmax);
+  return check_launch("prior_kernel");
+}
+
 }  // namespace
 
 extern "C" {
@@ -1493,11 +1784,15 @@ int32_t nais_forward(const nais_params_t* params, const int64_t* hist, int64_t b
   return rc;
 }
 
-size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k) {
+size_t nais_score_topk_workspace_size(const nais_params_t* params, int32_t num_users, int32_t k,
+                                      int32_t with_prior) {
   (void)k;
   if (!params || num_users <= 0) return 0;
   const int64_t nb = std::min<int64_t>(num_users, MAX_BATCH_USERS);
-  return (size_t)(nb * round_up(params->num_pois, 64) * (int64_t)sizeof(float));
+  const int64_t ld = round_up(params->num_pois, 64);
+  size_t bytes = (size_t)(nb * ld * (int64_t)sizeof(float));
+  if (with_prior) bytes += (size_t)(nb * ld * 8 + round_up(nb, 64) * 8);
+  return bytes;
 }
 
 int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, const int64_t* indices,
@@ -1519,8 +1814,8 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
     return fail(NAIS_E_INVALID, "region variants need region_of");
   if (params->variant == NAIS_VARIANT_REGION_DISTANCE && !coords && !latlon_mat)
     return fail(NAIS_E_INVALID, "region_distance needs coords or latlon_mat");
-  if (prior) return fail(NAIS_E_UNSUPPORTED, "power-law prior epilogue is not in ABI v1");
-  const size_t need = nais_score_topk_workspace_size(params, num_users, k);
+  if (prior && !prior->coords) return fail(NAIS_E_INVALID, "prior needs coords");
+  const size_t need = nais_score_topk_workspace_size(params, num_users, k, prior != nullptr);
   if (!workspace || workspace_bytes < need) return fail(NAIS_E_WORKSPACE, "workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   DevParams d;
@@ -1540,11 +1835,25 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
       NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0, nb,
                     region_of, coords, latlon_mat, scores, ld, nan_count, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(topk_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld,
-                       params->num_pois, k, out_ids + (int64_t)u0 * k,
-                       out_scores + (int64_t)u0 * k, short_count);
-    rc = check_launch("topk_kernel");
-    if (rc) return rc;
+    if (!prior) {
+      hipLaunchKernelGGL(topk_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld,
+                         params->num_pois, k, out_ids + (int64_t)u0 * k,
+                         out_scores + (int64_t)u0 * k, short_count);
+      rc = check_launch("topk_kernel");
+      if (rc) return rc;
+    } else {
+      const int64_t nbmax = std::min<int64_t>(num_users, MAX_BATCH_USERS);
+      double* G = reinterpret_cast<double*>(scores + nbmax * ld);
+      unsigned long long* gmax = reinterpret_cast<unsigned long long*>(G + nbmax * ld);
+      rc = launch_prior(prior->coords, params->num_pois, indptr, indices, users + u0, nb, prior->a,
+                        prior->b, G, ld, gmax, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL(topk_blend_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld, G, ld,
+                         gmax, params->num_pois, k, (float)(1.0 - prior->alpha), prior->alpha,
+                         out_ids + (int64_t)u0 * k, out_scores + (int64_t)u0 * k, short_count);
+      rc = check_launch("topk_blend_kernel");
+      if (rc) return rc;
+    }
   }
   return NAIS_OK;
 }
@@ -1605,6 +1914,41 @@ int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, 
     if (rc) return rc;
   }
   return NAIS_OK;
+}
+
+int32_t nais_powerlaw_prior(const double* coords, int64_t num_pois, const int64_t* indptr,
+                            const int64_t* indices, const int32_t* users, int32_t num_users, double a,
+                            double b, double* out, int64_t out_ld, double* out_max, void* stream) {
+  if (!coords || !indptr || !indices || !users || !out || !out_max || num_pois <= 0 ||
+      num_users < 0 || out_ld < num_pois)
+    return fail(NAIS_E_INVALID, "bad powerlaw_prior arguments");
+  if (num_pois > 65535ll * 256) return fail(NAIS_E_UNSUPPORTED, "num_pois too large");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_users - u0);
+    const int rc = launch_prior(coords, num_pois, indptr, indices, users + u0, nb, a, b,
+                                out + (int64_t)u0 * out_ld, out_ld,
+                                reinterpret_cast<unsigned long long*>(out_max + u0), st);
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_distance_histogram(const double* coords, const int64_t* indptr, const int64_t* indices,
+                                int64_t num_users, uint64_t* hist, int64_t nbins, uint64_t* overflow,
+                                void* stream) {
+  if (!coords || !indptr || !indices || !hist || !overflow || num_users < 0 || nbins <= 0)
+    return fail(NAIS_E_INVALID, "bad distance_histogram arguments");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint64_t) * nbins, st);
+  if (e == hipSuccess) e = hipMemsetAsync(overflow, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess) return fail(NAIS_E_HIP, std::string("memset: ") + hipGetErrorString(e));
+  if (num_users == 0) return NAIS_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>(num_users, 4096);
+  hipLaunchKernelGGL(distance_histogram_kernel, dim3(blocks), dim3(256), 0, st, coords, indptr, indices,
+                     num_users, reinterpret_cast<unsigned long long*>(hist), nbins,
+                     reinterpret_cast<unsigned long long*>(overflow));
+  return check_launch("distance_histogram_kernel");
 }
 
 int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim, const int64_t* idx,
