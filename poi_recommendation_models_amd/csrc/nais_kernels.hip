@@ -1514,15 +1514,34 @@ distance_histogram_kernel(const double* __restrict__ coords, const int64_t* __re
 // ---------------------------------------------------------------------------------------------
 // Standalone row gather (HBM roofline kernel): 16 B per lane, one row per dim/4 lanes.
 // ---------------------------------------------------------------------------------------------
+#ifndef NAIS_GATHER_UNROLL
+#define NAIS_GATHER_UNROLL 1
+#endif
+// Each thread moves NAIS_GATHER_UNROLL float4 pieces (from U different rows) per iteration: all
+// loads are issued before the stores, so every lane keeps U x 16 B in flight; rows are read once
+// and written once, so both sides use non-temporal (streaming) accesses.
+typedef float nf4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256)
-gather_rows_kernel(const float4* __restrict__ table, int q4, const int64_t* __restrict__ idx,
-                   int64_t m, float4* __restrict__ out) {
+gather_rows_kernel(const nf4* __restrict__ table, int q4, const int64_t* __restrict__ idx,
+                   int64_t m, nf4* __restrict__ out) {
+  constexpr int U = NAIS_GATHER_UNROLL;
   const int64_t total = m * q4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < total; i += U * stride) {
+    nf4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = i + u * stride;
+      const int64_t row = e / q4;
+      v[u] = __builtin_nontemporal_load(table + idx[row] * q4 + (e - row * q4));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], out + i + u * stride);
+  }
+  for (; i < total; i += stride) {
     const int64_t row = i / q4;
-    const int q = (int)(i - row * q4);
-    out[i] = table[idx[row] * q4 + q];
+    out[i] = table[idx[row] * q4 + (i - row * q4)];
   }
 }
 
@@ -1963,8 +1982,8 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim, const in
   const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
   if (vec)
     hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(table), dim / 4, idx, m,
-                       reinterpret_cast<float4*>(out));
+                       reinterpret_cast<const nf4*>(table), dim / 4, idx, m,
+                       reinterpret_cast<nf4*>(out));
   else
     hipLaunchKernelGGL(gather_rows_scalar_kernel, dim3((unsigned)blocks), dim3(256), 0, st, table,
                        dim, idx, m, out);
