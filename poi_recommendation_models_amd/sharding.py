@@ -98,3 +98,44 @@ def NAIS_validation_distributed(model, args, num_users, test_positive, val_posit
     precision_v, recall_v, hit_v = eval_metrics.evaluate_mp(val_positive, rec, k_list)
     precision_t, recall_t, hit_t = eval_metrics.evaluate_mp(test_positive, rec, k_list)
     return precision_v, recall_v, hit_v, precision_t, recall_t, hit_t
+
+
+def allgather_rows(local_rows, num_rows, group=None):
+    """Assemble a [num_rows, d] table from per-rank row blocks: rank r holds
+    rows [r*S, (r+1)*S) with S = ceil(num_rows / world) (the last block zero-padded), one
+    all_gather_into_tensor (a ring over xGMI with RCCL; ~7/8 of the table crosses each link)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    S = (num_rows + world - 1) // world
+    d = local_rows.shape[1]
+    block = torch.zeros(S, d, dtype=local_rows.dtype, device=local_rows.device)
+    block[:local_rows.shape[0]] = local_rows
+    full = torch.empty(S * world, d, dtype=local_rows.dtype, device=local_rows.device)
+    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
+        dist.all_gather_into_tensor(full, block, group=group)
+    else:
+        dist.all_gather(list(full.chunk(world)), block, group=group)
+    return full[:num_rows]
+
+
+def row_block(num_rows, rank, world):
+    """[start, end) of this rank's row block for allgather_rows."""
+    S = (num_rows + world - 1) // world
+    return min(rank * S, num_rows), min((rank + 1) * S, num_rows)
+
+
+def load_sharded_tables(model, init_rows, group=None):
+    """Each rank materialises only its 1/world slice of every POI-indexed table (init_rows(name,
+    start, end) -> [end-start, d] tensor), then the full tables are all-gathered; the small MLP
+    parameters are broadcast from rank 0. For tables too large to build on one host."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    for name in ("embed_history", "embed_target"):
+        w = getattr(model, name).weight
+        s, e = row_block(w.shape[0], rank, world)
+        local = init_rows(name, s, e).to(device=w.device, dtype=w.dtype)
+        with torch.no_grad():
+            w.copy_(allgather_rows(local, w.shape[0], group))
+    for n, p in model.named_parameters():
+        if not n.startswith(("embed_history", "embed_target")):
+            dist.broadcast(p.data, src=0, group=group)

@@ -75,3 +75,44 @@ def test_gather_topk_world2_matches_single_process():
     for rank, gi, gs in res:
         np.testing.assert_array_equal(gi, ref)
         assert not np.isnan(gs).any()
+
+
+def _worker_tables(rank, world, port, q):
+    import torch.distributed as dist
+    from poi_recommendation_models_amd.sharding import allgather_rows, load_sharded_tables, row_block
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, d = 1001, 8                                  # not divisible by world: padding path
+    full = torch.arange(P * d, dtype=torch.float32).reshape(P, d)
+    s, e = row_block(P, rank, world)
+    got = allgather_rows(full[s:e].clone(), P)
+    ok1 = torch.equal(got, full)
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.embed_history = torch.nn.Embedding(P, d)
+            self.embed_target = torch.nn.Embedding(P, d)
+            self.attn_layer1 = torch.nn.Linear(d, 4)
+    torch.manual_seed(rank)                         # ranks start with different MLP weights
+    m = M()
+    load_sharded_tables(m, lambda name, a, b: full[a:b] * (2 if name == "embed_target" else 1))
+    ok2 = torch.equal(m.embed_history.weight.data, full) and torch.equal(m.embed_target.weight.data, 2 * full)
+    q.put((rank, ok1, ok2, m.attn_layer1.weight.data.clone().numpy()))
+    dist.destroy_process_group()
+
+
+def test_sharded_table_allgather_world2():
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_tables, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(r[1] and r[2] for r in res)
+    np.testing.assert_array_equal(res[0][3], res[1][3])   # MLP broadcast from rank 0
