@@ -13,6 +13,9 @@
  *                       i.e. get_NAIS_batch_test* (batches.py:52-65, 110-139) + chunked forward + torch.topk
  *   nais_gather_rows    the embedding gather of model.py:64 (nn.Embedding -> index_select) as a standalone
  *                       HBM-roofline kernel
+ *   nais_train_*        one NAIS_basic training step (run.py:91-109): train-mode forward with dropout
+ *                       (model.py:22,40-89), backward of the attention pooling, dense embedding grads;
+ *                       nais_adagrad* = torch.optim.Adagrad's update (run.py:89)
  *
  * Conventions: every pointer is caller-owned DEVICE memory (e.g. torch tensor.data_ptr()); the library
  * never allocates, frees or copies caller memory, never synchronises, and issues all work on `stream`
@@ -31,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 3
+#define NAIS_ABI_VERSION 4
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -186,6 +189,56 @@ int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, 
  */
 int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
                          const int64_t* idx, int64_t m, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Training step of NAIS_basic on one get_NAIS_batch batch (batches.py:24-50):
+ * b rows (target[b], int64 POI ids) that all share ONE history hist[n] (int64, the user's positives;
+ * the reference repeats it b times, batches.py:30). Replaces, for this batch shape,
+ *   prediction = model(user_history, train_data)   (run.py:103; model.py:40-89 in train mode)
+ *   loss.backward()                                (run.py:105; BCELoss model.py:21)
+ * embed_dim in {8,16,32,64}, hidden <= 64, variant NAIS_VARIANT_BASIC (else NAIS_E_UNSUPPORTED).
+ *
+ * Dropout (nn.Dropout(dropout_p), model.py:22,71) keeps hidden unit i of pair (row c, item j) iff
+ * a counter hash of (seed, c*n + j, i) is >= dropout_p * 2^32 and scales kept units by 1/(1-p);
+ * dropout_p = 0 is eval-mode arithmetic. nais_dropout_mask() materialises the same mask
+ * (uint8 [b, n, hidden], 1 = kept) for tests.
+ *
+ * nais_train_forward: pred[b] = sigmoid(logit) (model.py:55); saved[2b] = (S, N) per row for the
+ *   backward; optional nan_count (+= rows whose logit is NaN, model.py:50-54).
+ * nais_train_backward: given grad_pred[b] = dL/dpred (e.g. from BCELoss's backward), ADDS the
+ *   gradients into grad_embed_history / grad_embed_target ([num_pois, embed_dim], dense, rows by
+ *   POI id), grad_w1 [hidden, embed_dim], grad_b1 [hidden], grad_w2 [hidden] (fp32 atomics: the
+ *   summation order is not fixed). Same params, hist, target, dropout_p and seed as the forward.
+ * -------------------------------------------------------------------------------------------- */
+size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n);
+
+int32_t nais_train_forward(const nais_params_t* params, const int64_t* hist, int64_t n,
+                           const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
+                           float* pred, float* saved, int32_t* nan_count, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
+int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, int64_t n,
+                            const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
+                            const float* pred, const float* saved, const float* grad_pred,
+                            float* grad_embed_history, float* grad_embed_target, float* grad_w1,
+                            float* grad_b1, float* grad_w2, void* stream);
+
+int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
+                          uint8_t* out, void* stream);
+
+/*
+ * torch.optim.Adagrad's update (run.py:89; lr_decay folded into clr = lr / (1 + (step-1) lr_decay)):
+ *   g' = g + weight_decay * p ; state += g' * g' ; p -= clr * g' / (sqrt(state) + eps)
+ * nais_adagrad: every element of a tensor of numel floats.
+ * nais_adagrad_rows: only rows[num_rows] (distinct) of a [*, dim] tensor, weight_decay 0. Rows
+ *   whose gradient is zero are left bit-identical by the dense update, so this equals
+ *   nais_adagrad when `rows` covers every row with a nonzero gradient.
+ */
+int32_t nais_adagrad(float* param, float* state_sum, const float* grad, int64_t numel, float clr,
+                     float weight_decay, float eps, void* stream);
+int32_t nais_adagrad_rows(float* param, float* state_sum, const float* grad, int32_t dim,
+                          const int64_t* rows, int64_t num_rows, float clr, float eps,
+                          void* stream);
 
 #ifdef __cplusplus
 }

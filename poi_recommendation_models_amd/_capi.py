@@ -12,14 +12,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE = 0, 1, 2
 FLAG_SIGMOID = 1
 
 EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_topk_workspace_size",
            "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_powerlaw_prior",
-           "nais_distance_histogram", "nais_gather_rows")
+           "nais_distance_histogram", "nais_gather_rows", "nais_train_workspace_size",
+           "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
+           "nais_adagrad_rows")
 
 
 class NaisParams(ctypes.Structure):
@@ -86,6 +88,21 @@ def load(path: str | None = None):
     lib.nais_distance_histogram.argtypes = [vp, vp, vp, i64, vp, i64, vp, vp]
     lib.nais_gather_rows.restype = i32
     lib.nais_gather_rows.argtypes = [vp, i64, i32, vp, i64, vp, vp]
+    f32, u64 = ctypes.c_float, ctypes.c_uint64
+    lib.nais_train_workspace_size.restype = sz
+    lib.nais_train_workspace_size.argtypes = [ctypes.POINTER(NaisParams), i64, i64]
+    lib.nais_train_forward.restype = i32
+    lib.nais_train_forward.argtypes = [ctypes.POINTER(NaisParams), vp, i64, vp, i64, f32, u64, vp, vp,
+                                       vp, vp, sz, vp]
+    lib.nais_train_backward.restype = i32
+    lib.nais_train_backward.argtypes = [ctypes.POINTER(NaisParams), vp, i64, vp, i64, f32, u64, vp, vp,
+                                        vp, vp, vp, vp, vp, vp, vp]
+    lib.nais_dropout_mask.restype = i32
+    lib.nais_dropout_mask.argtypes = [u64, i64, i64, i32, f32, vp, vp]
+    lib.nais_adagrad.restype = i32
+    lib.nais_adagrad.argtypes = [vp, vp, vp, i64, f32, f32, f32, vp]
+    lib.nais_adagrad_rows.restype = i32
+    lib.nais_adagrad_rows.argtypes = [vp, vp, vp, i32, vp, i64, f32, f32, vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

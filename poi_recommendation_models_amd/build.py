@@ -7,7 +7,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "nais_kernels.hip")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("nais_kernels.hip", "nais_train.hip")]
+SRC = SRCS[0]
 OUT = os.path.join(HERE, "libnais_hip.so")
 ARCH = os.environ.get("NAIS_OFFLOAD_ARCH", "gfx950")
 
@@ -20,14 +21,14 @@ def hipcc():
 
 
 def build(force=False, extra=()):
-    deps = [SRC, os.path.join(ROOT, "include", "nais.h")]
+    deps = [*SRCS, os.path.join(HERE, "csrc", "nais_internal.h"), os.path.join(ROOT, "include", "nais.h")]
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
     # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds/muls into v_pk_*_f32, which
     # cost more issue slots than two scalar ops beside MFMAs (cdna_hip_programming.md, price table);
     # measured +5 % on the split-fp16 catalog kernel (profiles/r1/ab_*.json).
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC, *extra]
+           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", *SRCS, *extra]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)

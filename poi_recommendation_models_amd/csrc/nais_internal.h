@@ -1,0 +1,9 @@
+// nais_internal.h -- declarations shared by the translation units of libnais_hip.so (not ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+// Records `msg` as the thread's nais_last_error() text and returns `code`.
+__attribute__((visibility("hidden"))) int nais_internal_fail(int code, const char* msg);
+// NAIS_E_HIP (with the HIP error text) if the last launch failed, else NAIS_OK.
+__attribute__((visibility("hidden"))) int nais_internal_check_launch(const char* what);

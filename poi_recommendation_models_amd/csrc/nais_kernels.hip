@@ -28,6 +28,7 @@
 #include <string>
 
 #include "nais.h"
+#include "nais_internal.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -1771,6 +1772,9 @@ int launch_prior(const double* coords, int64_t P, const int64_t* indptr, const i
 }
 
 }  // namespace
+
+int nais_internal_fail(int code, const char* msg) { return fail(code, msg); }
+int nais_internal_check_launch(const char* what) { return check_launch(what); }
 
 extern "C" {
 

@@ -1,0 +1,755 @@
+// nais_train.hip -- gfx950 kernels + C-ABI for the NAIS_basic training step.
+//
+// Reference: get_NAIS_batch (batches.py:24-50) builds b = (1 + num_ng) * n rows that all share the
+// user's n positives as their history; train_NAIS (run.py:91-109) then runs model.forward in train
+// mode (Dropout(0.5) on W1 x + b1, model.py:22,71), BCELoss (model.py:21,96-97), backward and
+// Adagrad (run.py:89,102-109).
+//
+// Per pair (row c, history item j), with x = h_j (.) t_c, u = W1 x + b1, v = u * m_cj (dropout
+// factors m in {0, 1/(1-p)}), z = ReLU(v), a = w2 . z, e = exp(a) [h_j != t_c], s = h_j . t_c:
+//   S_c = sum_j e, N_c = sum_j e s, logit_c = N_c / S_c^beta, pred_c = sigmoid(logit_c).
+// Given g_c = dL/dlogit_c (from dL/dpred via the sigmoid), the backward of model.py:57-89 is
+//   ds = g e / S^beta                      (dlogit/ds_cj)
+//   da = ds (s - beta N / S)               (dlogit/de_cj times de/da = e)
+//   du = da w2 [v > 0] * scale             (ReLU + dropout backward, scale = 1/(1-p) if kept)
+//   dW1 += du x^T, db1 += du, dw2 += da z, dx = W1^T du, r = dx + ds
+//   dh_j += r (.) t_c, dt_c += r (.) h_j.
+// Both kernels recompute u from the embeddings (one exact-fp32 MFMA chain, as the scorer), so no
+// [b, n, H] tensor is ever stored; dropout factors come from a counter hash of (seed, c*n+j, i),
+// so the forward and backward launches see the same mask without storing it.
+//
+// MFMA layout (v_mfma_f32_32x32x2_f32, 32 rows per wave as the B/C columns):
+//   forward  acc[hb] (32 hidden x 32 rows) += W1[hb block][K pair] x x[K pair][rows]
+//   dx       dx[db]  (32 dims x 32 rows)   += W1^T[db block][K pair] x du[K pair][rows]
+//            -- du is fed straight from the forward accumulator registers: K-step (hb, r) takes
+//               hidden unit crow(hb, r, hh), so no data movement is needed. The forward K order
+//               over embedding dims is chosen as the C layout of dx (kdim below), so the lane that
+//               supplies x[dim] holds dx[dim] afterwards.
+//   dW1      per item, the 128 rows of du and x go through LDS ([row][hidden], [row][dim]) and
+//            each wave accumulates its 32x32 tiles of dW1 with K = the workgroup's 128 rows.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+
+#include "nais.h"
+#include "nais_internal.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int TW = 4;               // waves per training workgroup (one per SIMD)
+constexpr int TTHREADS = TW * 64;
+constexpr int TROWS = TW * 32;      // batch rows per workgroup: 32 per wave (the MFMA columns)
+constexpr int MAX_JS = 32;          // history items per slice (grid.y)
+
+__device__ __forceinline__ floatx16 mfma(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// row held in accumulator register r of 32-row block blk by lane half hh (32x32 C layout)
+__device__ __forceinline__ int crow(int blk, int r, int hh) {
+  return blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+}
+// embedding dim carried by K-step s of the forward MFMA in lane half hh (= C layout of dx)
+__device__ __forceinline__ int kdim(int s, int hh) { return crow(s >> 4, s & 15, hh); }
+// first of the 4 consecutive dims of K-steps 4g..4g+3
+__device__ __forceinline__ int kdim4(int g, int hh) { return 32 * (g >> 2) + 8 * (g & 3) + 4 * hh; }
+
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Dropout as in nn.Dropout(p) (model.py:22): keep with probability 1-p and scale by 1/(1-p).
+// The draw for hidden unit i of pair (c, j) is a hash of (seed, c*n+j, i) -- same bits in every
+// kernel, no mask storage. Distributionally the reference's Bernoulli mask, not its RNG stream
+// (the parity tests inject the mask through nais_dropout_mask).
+struct Drop {
+  uint32_t s0, s1, thr;
+  float scale;
+  int on;
+  __device__ __forceinline__ uint32_t key(uint32_t pair) const { return mix32(pair ^ s0); }
+  __device__ __forceinline__ float factor(uint32_t k, int i) const {
+    return mix32((k + uint32_t(i) * 0x9e3779b9u) ^ s1) >= thr ? scale : 0.f;
+  }
+};
+
+Drop make_drop(float p, uint64_t seed) {
+  Drop d;
+  d.s0 = uint32_t(seed);
+  d.s1 = mix32(uint32_t(seed >> 32) ^ 0x5bd1e995u);
+  d.on = p > 0.f;
+  if (p >= 1.f) {
+    d.thr = 0;
+    d.scale = 0.f;
+  } else {
+    const double t = double(p) * 4294967296.0;
+    d.thr = t >= 4294967295.0 ? 0xffffffffu : uint32_t(t);
+    d.scale = float(1.0 / (1.0 - double(p)));
+  }
+  return d;
+}
+
+struct TrainArgs {
+  const float* eh;
+  const float* et;
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const int64_t* hist;
+  const int64_t* target;
+  int64_t b, n;
+  int H, D;
+  float beta;
+  int js;  // history items per slice (blockIdx.y)
+  Drop drop;
+};
+
+// LDS layout (floats). W1 is kept twice: row-major for the forward A operand (a lane reads 4
+// consecutive dims of its hidden row) and transposed for the dx A operand (4 consecutive hidden
+// units of its dim row); rows are padded by 4 floats so 16-byte reads of 32 rows hit distinct banks.
+template <int DH, int HB>
+struct TL {
+  static constexpr int D = 2 * DH;
+  static constexpr int DW = D < 32 ? 32 : D;  // dims padded to one 32-row MFMA block
+  static constexpr int HW = 32 * HB;
+  static constexpr int W1P = DW + 4, W1TP = HW + 4, XP = DW + 4, UP = HW + 4;
+  static constexpr int O_W1 = 0;
+  static constexpr int O_B1 = O_W1 + HW * W1P;
+  static constexpr int O_W2 = O_B1 + HW;
+  static constexpr int O_H = O_W2 + HW;             // history slice [MAX_JS][D]
+  static constexpr int FWD = O_H + MAX_JS * D;
+  static constexpr int O_W1T = FWD;                 // backward only from here on
+  static constexpr int O_DH = O_W1T + DW * W1TP;    // dh accumulator [MAX_JS][D]
+  static constexpr int O_X = O_DH + MAX_JS * D;     // x of the workgroup's rows [TROWS][XP]
+  static constexpr int O_U = O_X + TROWS * XP;      // du of the workgroup's rows [TROWS][UP]
+  static constexpr int BWD = O_U + TROWS * UP;
+};
+
+template <int DH, int HB>
+__device__ void stage_w(const TrainArgs& a, float* L, int tid, bool transposed) {
+  using T = TL<DH, HB>;
+  for (int f = tid; f < T::HW * T::DW; f += TTHREADS) {
+    const int i = f / T::DW, k = f % T::DW;
+    const float v = (i < a.H && k < a.D) ? a.w1[(int64_t)i * a.D + k] : 0.f;
+    L[T::O_W1 + i * T::W1P + k] = v;
+    if (transposed) L[T::O_W1T + k * T::W1TP + i] = v;
+  }
+  for (int i = tid; i < T::HW; i += TTHREADS) {
+    L[T::O_B1 + i] = i < a.H ? a.b1[i] : 0.f;
+    L[T::O_W2 + i] = i < a.H ? a.w2[i] : 0.f;
+  }
+}
+
+template <int DH, int HB>
+__device__ void stage_hist(const TrainArgs& a, float* L, int tid, int64_t j0, int nj) {
+  using T = TL<DH, HB>;
+  constexpr int D = T::D;
+  for (int f = tid; f < nj * (D / 4); f += TTHREADS) {
+    const int jj = f / (D / 4), q = f % (D / 4);
+    reinterpret_cast<float4*>(L + T::O_H)[f] =
+        reinterpret_cast<const float4*>(a.eh + a.hist[j0 + jj] * D)[q];
+  }
+}
+
+// t_c in K order (kdim) for this lane; zeros for rows past the batch.
+template <int DH>
+__device__ __forceinline__ void load_target(const TrainArgs& a, int64_t tgt, bool active, int hh,
+                                            float (&t)[DH]) {
+#pragma unroll
+  for (int g = 0; g < DH / 4; ++g) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (active) v = *reinterpret_cast<const float4*>(a.et + tgt * (2 * DH) + kdim4(g, hh));
+    t[4 * g] = v.x;
+    t[4 * g + 1] = v.y;
+    t[4 * g + 2] = v.z;
+    t[4 * g + 3] = v.w;
+  }
+}
+
+// Forward of one pair for the lane's row: h (K order), x = t (.) h, acc = dropout(b1 + W1 x)
+// (post-dropout v), s = h . t and the attention logit a (both joined over the two lane halves).
+template <int DH, int HB>
+__device__ __forceinline__ void pair_forward(const TrainArgs& ar, const float* L, const float* hrow,
+                                             const float (&t)[DH], int lane, uint32_t pair,
+                                             float (&h)[DH], float (&x)[DH], floatx16 (&acc)[HB],
+                                             float& sdot, float& a) {
+  using T = TL<DH, HB>;
+  const int hh = lane >> 5, ci = lane & 31;
+  float sp = 0.f;
+#pragma unroll
+  for (int g = 0; g < DH / 4; ++g) {
+    const float4 h4 = *reinterpret_cast<const float4*>(hrow + kdim4(g, hh));
+    h[4 * g] = h4.x;
+    h[4 * g + 1] = h4.y;
+    h[4 * g + 2] = h4.z;
+    h[4 * g + 3] = h4.w;
+  }
+#pragma unroll
+  for (int s = 0; s < DH; ++s) {
+    x[s] = t[s] * h[s];
+    sp += x[s];
+  }
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[hb][r] = L[T::O_B1 + crow(hb, r, hh)];
+    const float* wrow = L + T::O_W1 + (32 * hb + ci) * T::W1P;
+#pragma unroll
+    for (int g = 0; g < DH / 4; ++g) {
+      const float4 w = *reinterpret_cast<const float4*>(wrow + kdim4(g, hh));
+      acc[hb] = mfma(w.x, x[4 * g], acc[hb]);
+      acc[hb] = mfma(w.y, x[4 * g + 1], acc[hb]);
+      acc[hb] = mfma(w.z, x[4 * g + 2], acc[hb]);
+      acc[hb] = mfma(w.w, x[4 * g + 3], acc[hb]);
+    }
+  }
+  float ap = 0.f;
+  const uint32_t k = ar.drop.on ? ar.drop.key(pair) : 0u;
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = crow(hb, r, hh);
+      float v = acc[hb][r];
+      if (ar.drop.on) v *= ar.drop.factor(k, i);
+      acc[hb][r] = v;
+      ap = fmaf(L[T::O_W2 + i], fmaxf(v, 0.f), ap);
+    }
+  }
+  a = ap + __shfl_xor(ap, 32);
+  sdot = sp + __shfl_xor(sp, 32);
+}
+
+// Sum of v[] over the 32 lanes of each lane half (a reduce-scatter butterfly: NV-1 + 5-log2(NV)
+// shuffles instead of 5 NV). Afterwards lane (ci, hh) holds the total of entry ci >> (5 - log2 NV).
+template <int NV, int CNT, int O>
+__device__ __forceinline__ void rs_step(float (&v)[NV], int lane) {
+  if constexpr (O > 0) {
+    if constexpr (CNT > 1) {
+      constexpr int HL = CNT / 2;
+      const bool up = lane & O;
+#pragma unroll
+      for (int m = 0; m < HL; ++m) {
+        const float send = up ? v[m] : v[m + HL];
+        const float keep = up ? v[m + HL] : v[m];
+        v[m] = keep + __shfl_xor(send, O);
+      }
+      rs_step<NV, HL, O / 2>(v, lane);
+    } else {
+      v[0] += __shfl_xor(v[0], O);
+      rs_step<NV, 1, O / 2>(v, lane);
+    }
+  }
+}
+template <int NV>
+__device__ __forceinline__ float half_reduce_scatter(float (&v)[NV], int lane) {
+  rs_step<NV, NV, 16>(v, lane);
+  return v[0];
+}
+
+template <int NV>
+constexpr int log2c() {
+  return NV <= 1 ? 0 : 1 + log2c<NV / 2>();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward: grid (ceil(b / 128), ceil(n / js)); per (row, slice) the partial S and N.
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB>
+__global__ void __launch_bounds__(TTHREADS)
+train_forward_kernel(TrainArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
+  using T = TL<DH, HB>;
+  extern __shared__ float4 lds4[];
+  float* L = reinterpret_cast<float*>(lds4);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5;
+  const int64_t c = int64_t(blockIdx.x) * TROWS + w * 32 + (lane & 31);
+  const int64_t j0 = int64_t(blockIdx.y) * a.js;
+  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
+  const bool active = c < a.b;
+  const int64_t tgt = active ? a.target[c] : -1;
+  stage_w<DH, HB>(a, L, tid, false);
+  stage_hist<DH, HB>(a, L, tid, j0, nj);
+  float t[DH];
+  load_target<DH>(a, tgt, active, hh, t);
+  __syncthreads();
+  float S = 0.f, N = 0.f;
+  for (int jj = 0; jj < nj; ++jj) {
+    float h[DH], x[DH], sdot, at;
+    floatx16 acc[HB];
+    pair_forward<DH, HB>(a, L, L + T::O_H + jj * T::D, t, lane, uint32_t(c * a.n + j0 + jj), h, x,
+                         acc, sdot, at);
+    const float e = expf(at) * (a.hist[j0 + jj] != tgt ? 1.f : 0.f);  // model.py:74-78
+    S += e;
+    N = fmaf(e, sdot, N);
+  }
+  if (active && hh == 0) {
+    Sp[int64_t(blockIdx.y) * a.b + c] = S;
+    Np[int64_t(blockIdx.y) * a.b + c] = N;
+  }
+}
+
+// S, N over the slices -> logit (model.py:79-89), pred = sigmoid (model.py:55), NaN count.
+__global__ void train_finalize_kernel(const float* __restrict__ Sp, const float* __restrict__ Np,
+                                      int ns, int64_t b, int64_t n, float beta, float* pred,
+                                      float* saved, int32_t* nan_count) {
+  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (c >= b) return;
+  float S = 0.f, N = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    S += Sp[int64_t(s) * b + c];
+    N += Np[int64_t(s) * b + c];
+  }
+  float logit = 0.f;  // empty history: the sum over n is 0
+  if (n > 0) logit = N / ((beta == 0.5f) ? sqrtf(S) : powf(S, beta));
+  pred[c] = 1.0f / (1.0f + expf(-logit));
+  saved[c] = S;
+  saved[b + c] = N;
+  if (nan_count && logit != logit) atomicAdd(nan_count, 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward: same grid as the forward. Gradients are ADDED into the caller's buffers (fp32
+// atomics: the dense embedding grads by POI id, so repeated ids are summed as index_add does).
+// ---------------------------------------------------------------------------------------------
+template <int DH, int HB>
+__global__ void __launch_bounds__(TTHREADS, 1)
+train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
+                      const float* __restrict__ gpred, float* __restrict__ g_eh,
+                      float* __restrict__ g_et, float* __restrict__ g_w1, float* __restrict__ g_b1,
+                      float* __restrict__ g_w2) {
+  using T = TL<DH, HB>;
+  constexpr int D = T::D;
+  constexpr int DB = (DH + 15) / 16;             // 32-dim blocks of dx / dW1 columns
+  constexpr int NT = HB * DB;                    // 32x32 tiles of dW1
+  constexpr int TPW = (NT + TW - 1) / TW;        // tiles per wave
+  constexpr int SHD = 5 - log2c<DH>();           // reduce-scatter entry shift (dims)
+  constexpr int SHH = 5 - log2c<16 * HB>();      // reduce-scatter entry shift (hidden)
+  extern __shared__ float4 lds4[];
+  float* L = reinterpret_cast<float*>(lds4);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, ci = lane & 31;
+  const int64_t c = int64_t(blockIdx.x) * TROWS + w * 32 + ci;
+  const int64_t j0 = int64_t(blockIdx.y) * a.js;
+  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
+  const bool active = c < a.b;
+  const int64_t tgt = active ? a.target[c] : -1;
+
+  stage_w<DH, HB>(a, L, tid, true);
+  stage_hist<DH, HB>(a, L, tid, j0, nj);
+  for (int f = tid; f < MAX_JS * D; f += TTHREADS) L[T::O_DH + f] = 0.f;
+  for (int f = tid; f < TROWS * T::XP; f += TTHREADS) L[T::O_X + f] = 0.f;  // dims >= D stay 0
+  float t[DH];
+  load_target<DH>(a, tgt, active, hh, t);
+
+  // per-row scalars: g = dL/dlogit (sigmoid backward of the reference: grad * (1 - y) * y)
+  float gl = 0.f, bns = 0.f;
+  if (active) {
+    const float p = pred[c], S = saved[c], N = saved[a.b + c];
+    const float g = gpred[c] * (1.f - p) * p;
+    gl = g / ((a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta));
+    bns = a.beta * N / S;
+  }
+  const float sc = a.drop.on ? a.drop.scale : 1.f;
+
+  float dt[DH];
+#pragma unroll
+  for (int s = 0; s < DH; ++s) dt[s] = 0.f;
+  float gb1[16 * HB], gw2[16 * HB];
+#pragma unroll
+  for (int q = 0; q < 16 * HB; ++q) gb1[q] = gw2[q] = 0.f;
+  floatx16 gw[TPW];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gw[tt][r] = 0.f;
+  __syncthreads();
+
+  float* xrow = L + T::O_X + (w * 32 + ci) * T::XP;
+  float* urow = L + T::O_U + (w * 32 + ci) * T::UP;
+  for (int jj = 0; jj < nj; ++jj) {
+    float h[DH], x[DH], sdot, at;
+    floatx16 acc[HB];
+    pair_forward<DH, HB>(a, L, L + T::O_H + jj * D, t, lane, uint32_t(c * a.n + j0 + jj), h, x,
+                         acc, sdot, at);
+    const float e = expf(at) * (a.hist[j0 + jj] != tgt ? 1.f : 0.f);
+    const float ds = gl * e;
+    const float da = ds * (sdot - bns);
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = crow(hb, r, hh);
+        const float v = acc[hb][r];
+        const float wi = L[T::O_W2 + i];
+        gw2[hb * 16 + r] = fmaf(da, fmaxf(v, 0.f), gw2[hb * 16 + r]);
+        const float du = v > 0.f ? da * wi * sc : 0.f;
+        gb1[hb * 16 + r] += du;
+        acc[hb][r] = du;
+      }
+    }
+    // x and du of this row into LDS for the dW1 product (K = the workgroup's rows)
+#pragma unroll
+    for (int g = 0; g < DH / 4; ++g)
+      *reinterpret_cast<float4*>(xrow + kdim4(g, hh)) =
+          make_float4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(urow + 32 * hb + 8 * g + 4 * hh) =
+            make_float4(acc[hb][4 * g], acc[hb][4 * g + 1], acc[hb][4 * g + 2], acc[hb][4 * g + 3]);
+
+    // dx = W1^T du, du taken from the accumulator registers as the B operand
+    floatx16 dx[DB];
+#pragma unroll
+    for (int db = 0; db < DB; ++db) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dx[db][r] = 0.f;
+      const float* wt = L + T::O_W1T + (32 * db + ci) * T::W1TP;
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 wv = *reinterpret_cast<const float4*>(wt + 32 * hb + 8 * g + 4 * hh);
+          dx[db] = mfma(wv.x, acc[hb][4 * g], dx[db]);
+          dx[db] = mfma(wv.y, acc[hb][4 * g + 1], dx[db]);
+          dx[db] = mfma(wv.z, acc[hb][4 * g + 2], dx[db]);
+          dx[db] = mfma(wv.w, acc[hb][4 * g + 3], dx[db]);
+        }
+    }
+    float vh[DH];
+#pragma unroll
+    for (int s = 0; s < DH; ++s) {
+      const float r = dx[s >> 4][s & 15] + ds;
+      dt[s] = fmaf(r, h[s], dt[s]);
+      vh[s] = r * t[s];
+    }
+    const float hsum = half_reduce_scatter<DH>(vh, lane);
+    if ((ci & ((1 << SHD) - 1)) == 0) atomicAdd(&L[T::O_DH + jj * D + kdim(ci >> SHD, hh)], hsum);
+    __syncthreads();
+    // dW1 tiles: A = du^T rows (hidden), B = x rows (dims), K over the 128 rows
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int tile = w + TW * tt;
+      if (tile < NT) {
+        const int ib = tile / DB, kb = tile % DB;
+        const float* ua = L + T::O_U + 32 * ib + ci;
+        const float* xb = L + T::O_X + 32 * kb + ci;
+#pragma unroll 8
+        for (int kk = 0; kk < TROWS / 2; ++kk) {
+          const int row = 2 * kk + hh;
+          gw[tt] = mfma(ua[row * T::UP], xb[row * T::XP], gw[tt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- flush: dW1, db1, dw2, dt (per row), dh (per history item)
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    const int tile = w + TW * tt;
+    if (tile < NT) {
+      const int ib = tile / DB, kb = tile % DB;
+      const int col = 32 * kb + ci;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = crow(ib, r, hh);
+        if (row < a.H && col < D) unsafeAtomicAdd(&g_w1[row * D + col], gw[tt][r]);
+      }
+    }
+  }
+  {
+    const float sb = half_reduce_scatter<16 * HB>(gb1, lane);
+    const float sw = half_reduce_scatter<16 * HB>(gw2, lane);
+    if ((ci & ((1 << SHH) - 1)) == 0) {
+      const int m = ci >> SHH;
+      const int i = crow(m >> 4, m & 15, hh);
+      if (i < a.H) {
+        unsafeAtomicAdd(&g_b1[i], sb);
+        unsafeAtomicAdd(&g_w2[i], sw);
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int s = 0; s < DH; ++s) unsafeAtomicAdd(&g_et[tgt * D + kdim(s, hh)], dt[s]);
+  }
+  __syncthreads();
+  for (int f = tid; f < nj * D; f += TTHREADS)
+    unsafeAtomicAdd(&g_eh[a.hist[j0 + f / D] * D + f % D], L[T::O_DH + f]);
+}
+
+__global__ void dropout_mask_kernel(Drop d, int64_t b, int64_t n, int H, uint8_t* out) {
+  const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= b * n * H) return;
+  const int i = int(idx % H);
+  const int64_t pair = idx / H;
+  out[idx] = d.on ? (d.factor(d.key(uint32_t(pair)), i) != 0.f) : 1;
+}
+
+// torch.optim.Adagrad (run.py:89) update of one tensor:
+//   g += wd p ; state += g g ; p -= clr g / (sqrt(state) + eps)
+__global__ void adagrad_kernel(float* __restrict__ p, float* __restrict__ st,
+                               const float* __restrict__ g, int64_t numel, float clr, float wd,
+                               float eps) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < numel;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    float gi = g[i];
+    const float pi = p[i];
+    if (wd != 0.f) gi = gi + wd * pi;
+    const float si = st[i] + gi * gi;
+    st[i] = si;
+    p[i] = pi + (-clr) * (gi / (sqrtf(si) + eps));
+  }
+}
+
+// The same update restricted to `rows` of a [*, dim] tensor (rows distinct). With weight_decay 0
+// a row whose gradient is zero is left bit-identical by the dense update (state += 0, p -= 0),
+// so this equals the dense step when `rows` covers every row with a nonzero gradient.
+__global__ void adagrad_rows_kernel(float* __restrict__ p, float* __restrict__ st,
+                                    const float* __restrict__ g, int dim,
+                                    const int64_t* __restrict__ rows, int64_t nrows, float clr,
+                                    float eps) {
+  const int64_t total = nrows * dim;
+  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < total;
+       f += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = rows[f / dim] * dim + f % dim;
+    const float gi = g[i];
+    const float si = st[i] + gi * gi;
+    st[i] = si;
+    p[i] = p[i] + (-clr) * (gi / (sqrtf(si) + eps));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+struct TShape {
+  int DH, HB;
+};
+
+int tvalidate(const nais_params_t* p, TShape* sh) {
+  if (!p) return nais_internal_fail(NAIS_E_INVALID, "params is NULL");
+  if (p->variant != NAIS_VARIANT_BASIC)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training step: only NAIS_basic is supported");
+  if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
+    return nais_internal_fail(NAIS_E_INVALID, "missing parameter pointer");
+  const int D = p->embed_dim;
+  if (p->item_dim != D || p->din != D)
+    return nais_internal_fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
+  if (D != 8 && D != 16 && D != 32 && D != 64)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training step: embed_dim must be 8, 16, 32 or 64");
+  if (p->hidden <= 0 || p->hidden > 64)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training step: hidden must be in [1, 64]");
+  sh->DH = D / 2;
+  sh->HB = p->hidden > 32 ? 2 : 1;
+  return NAIS_OK;
+}
+
+TrainArgs targs(const nais_params_t* p, const int64_t* hist, int64_t n, const int64_t* target,
+                int64_t b, int js, float dropout_p, uint64_t seed) {
+  TrainArgs a;
+  a.eh = p->embed_history;
+  a.et = p->embed_target;
+  a.w1 = p->w1;
+  a.b1 = p->b1;
+  a.w2 = p->w2;
+  a.hist = hist;
+  a.target = target;
+  a.b = b;
+  a.n = n;
+  a.H = p->hidden;
+  a.D = p->embed_dim;
+  a.beta = p->beta;
+  a.js = js;
+  a.drop = make_drop(dropout_p, seed);
+  return a;
+}
+
+// Items per slice: about `per_cu` workgroups per CU over the 256 CUs, at most MAX_JS.
+int slice_items(int64_t b, int64_t n, int per_cu) {
+  const int64_t rb = (b + TROWS - 1) / TROWS;
+  const int64_t want = 256 * per_cu;
+  int64_t js = (n * rb + want - 1) / want;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(MAX_JS, js));
+}
+constexpr int FWD_PER_CU = 4, BWD_PER_CU = 1;
+
+template <typename K>
+void set_lds(K kern, size_t bytes) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int DH, int HB>
+int launch_train_forward(const TrainArgs& a, float* Sp, float* Np, hipStream_t st) {
+  const size_t lds = size_t(TL<DH, HB>::FWD) * 4;
+  auto kern = train_forward_kernel<DH, HB>;
+  static bool once = (set_lds(kern, lds), true);
+  (void)once;
+  dim3 grid((unsigned)((a.b + TROWS - 1) / TROWS), (unsigned)((a.n + a.js - 1) / a.js));
+  hipLaunchKernelGGL(kern, grid, dim3(TTHREADS), lds, st, a, Sp, Np);
+  return nais_internal_check_launch("train_forward_kernel");
+}
+
+template <int DH, int HB>
+int launch_train_backward(const TrainArgs& a, const float* saved, const float* pred,
+                          const float* gpred, float* g_eh, float* g_et, float* g_w1, float* g_b1,
+                          float* g_w2, hipStream_t st) {
+  const size_t lds = size_t(TL<DH, HB>::BWD) * 4;
+  auto kern = train_backward_kernel<DH, HB>;
+  static bool once = (set_lds(kern, lds), true);
+  (void)once;
+  dim3 grid((unsigned)((a.b + TROWS - 1) / TROWS), (unsigned)((a.n + a.js - 1) / a.js));
+  hipLaunchKernelGGL(kern, grid, dim3(TTHREADS), lds, st, a, saved, pred, gpred, g_eh, g_et, g_w1,
+                     g_b1, g_w2);
+  return nais_internal_check_launch("train_backward_kernel");
+}
+
+#define NAIS_TRAIN_DISPATCH(FN, SH, ...)                        \
+  switch ((SH).DH * 4 + (SH).HB) {                              \
+    case 4 * 4 + 1: rc = FN<4, 1>(__VA_ARGS__); break;          \
+    case 4 * 4 + 2: rc = FN<4, 2>(__VA_ARGS__); break;          \
+    case 8 * 4 + 1: rc = FN<8, 1>(__VA_ARGS__); break;          \
+    case 8 * 4 + 2: rc = FN<8, 2>(__VA_ARGS__); break;          \
+    case 16 * 4 + 1: rc = FN<16, 1>(__VA_ARGS__); break;        \
+    case 16 * 4 + 2: rc = FN<16, 2>(__VA_ARGS__); break;        \
+    case 32 * 4 + 1: rc = FN<32, 1>(__VA_ARGS__); break;        \
+    default: rc = FN<32, 2>(__VA_ARGS__); break;                \
+  }
+
+int check_batch(const int64_t* hist, int64_t n, const int64_t* target, int64_t b) {
+  if (b < 0 || n < 0) return nais_internal_fail(NAIS_E_INVALID, "negative b or n");
+  if (b > 0 && !target) return nais_internal_fail(NAIS_E_INVALID, "missing target");
+  if (n > 0 && !hist) return nais_internal_fail(NAIS_E_INVALID, "missing history");
+  if ((b + TROWS - 1) / TROWS > 0x7fffffff) return nais_internal_fail(NAIS_E_UNSUPPORTED, "b too large");
+  return NAIS_OK;
+}
+
+int hip_rc(hipError_t e, const char* what) {
+  if (e == hipSuccess) return NAIS_OK;
+  return nais_internal_fail(NAIS_E_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
+  (void)params;
+  if (b <= 0 || n <= 0) return 0;
+  const int js = slice_items(b, n, FWD_PER_CU);
+  const int64_t ns = (n + js - 1) / js;
+  return size_t(2 * ns * b) * sizeof(float);
+}
+
+int32_t nais_train_forward(const nais_params_t* params, const int64_t* hist, int64_t n,
+                           const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
+                           float* pred, float* saved, int32_t* nan_count, void* workspace,
+                           size_t workspace_bytes, void* stream) {
+  TShape sh;
+  int rc = tvalidate(params, &sh);
+  if (rc) return rc;
+  if ((rc = check_batch(hist, n, target, b))) return rc;
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  if (b == 0) return NAIS_OK;
+  if (!pred || !saved) return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) {  // no history: logit 0 for every row, S = N = 0
+    hipLaunchKernelGGL(train_finalize_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
+                       nullptr, nullptr, 0, b, n, params->beta, pred, saved, nan_count);
+    return nais_internal_check_launch("train_finalize_kernel");
+  }
+  const int js = slice_items(b, n, FWD_PER_CU);
+  const int64_t ns = (n + js - 1) / js;
+  if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  if (!workspace || workspace_bytes < nais_train_workspace_size(params, b, n))
+    return nais_internal_fail(NAIS_E_WORKSPACE, "workspace too small (nais_train_workspace_size)");
+  float* Sp = static_cast<float*>(workspace);
+  float* Np = Sp + ns * b;
+  const TrainArgs a = targs(params, hist, n, target, b, js, dropout_p, seed);
+  NAIS_TRAIN_DISPATCH(launch_train_forward, sh, a, Sp, Np, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(train_finalize_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
+                     Sp, Np, (int)ns, b, n, params->beta, pred, saved, nan_count);
+  return nais_internal_check_launch("train_finalize_kernel");
+}
+
+int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, int64_t n,
+                            const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
+                            const float* pred, const float* saved, const float* grad_pred,
+                            float* grad_embed_history, float* grad_embed_target, float* grad_w1,
+                            float* grad_b1, float* grad_w2, void* stream) {
+  TShape sh;
+  int rc = tvalidate(params, &sh);
+  if (rc) return rc;
+  if ((rc = check_batch(hist, n, target, b))) return rc;
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  if (b == 0 || n == 0) return NAIS_OK;  // no history: the logit is constant, all grads 0
+  if (!pred || !saved || !grad_pred || !grad_embed_history || !grad_embed_target || !grad_w1 ||
+      !grad_b1 || !grad_w2)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved/grad pointer");
+  const int js = slice_items(b, n, BWD_PER_CU);
+  if ((n + js - 1) / js > 65535)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  const TrainArgs a = targs(params, hist, n, target, b, js, dropout_p, seed);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  NAIS_TRAIN_DISPATCH(launch_train_backward, sh, a, saved, pred, grad_pred, grad_embed_history,
+                      grad_embed_target, grad_w1, grad_b1, grad_w2, st);
+  return rc;
+}
+
+int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
+                          uint8_t* out, void* stream) {
+  if (b < 0 || n < 0 || hidden <= 0) return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  const int64_t total = b * n * hidden;
+  if (total == 0) return NAIS_OK;
+  if (!out) return nais_internal_fail(NAIS_E_INVALID, "out is NULL");
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), make_drop(dropout_p, seed), b, n,
+                     (int)hidden, out);
+  return nais_internal_check_launch("dropout_mask_kernel");
+}
+
+int32_t nais_adagrad(float* param, float* state_sum, const float* grad, int64_t numel, float clr,
+                     float weight_decay, float eps, void* stream) {
+  if (numel < 0) return nais_internal_fail(NAIS_E_INVALID, "negative numel");
+  if (numel == 0) return NAIS_OK;
+  if (!param || !state_sum || !grad) return nais_internal_fail(NAIS_E_INVALID, "NULL tensor");
+  const int64_t blocks = std::min<int64_t>((numel + 255) / 256, 2048 * 4);
+  hipLaunchKernelGGL(adagrad_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), param, state_sum, grad, numel, clr,
+                     weight_decay, eps);
+  return nais_internal_check_launch("adagrad_kernel");
+}
+
+int32_t nais_adagrad_rows(float* param, float* state_sum, const float* grad, int32_t dim,
+                          const int64_t* rows, int64_t num_rows, float clr, float eps,
+                          void* stream) {
+  if (num_rows < 0 || dim <= 0) return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (num_rows == 0) return NAIS_OK;
+  if (!param || !state_sum || !grad || !rows)
+    return nais_internal_fail(NAIS_E_INVALID, "NULL tensor");
+  const int64_t total = num_rows * dim;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 2048 * 4);
+  hipLaunchKernelGGL(adagrad_rows_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), param, state_sum, grad, dim, rows,
+                     num_rows, clr, eps);
+  return nais_internal_check_launch("adagrad_rows_kernel");
+}
+
+}  // extern "C"

@@ -10,9 +10,15 @@ signatures follow the reference:
 
 `forward` evaluates attention_network + sigmoid on the device in one fused kernel
 (`nais_forward`); there is no CPU path: inputs must live on the ROCm device that holds the
-parameters, otherwise a RuntimeError is raised. The modules implement eval-mode semantics
-(Dropout = identity, as under `model.eval()` in every reference validation loop). The training
-step (dropout + backward) is not built yet: forward in training mode raises.
+parameters, otherwise a RuntimeError is raised. In eval mode Dropout is the identity (as under
+`model.eval()` in every reference validation loop).
+
+Training (run.py:91-109): `NAIS_basic.forward` in train mode runs
+`nais_train_forward` (Dropout(p) on W1 x + b1, model.py:71) inside an autograd Function whose
+backward is `nais_train_backward`, so the reference's loop -- forward, `loss_func`, `backward()`,
+optimizer step -- runs unchanged. The batch must be get_NAIS_batch's shape (batches.py:24-50):
+every row shares one history (checked; per-row histories raise). The region variants train on
+the eval-only path for now (train-mode forward raises NotImplementedError).
 """
 from __future__ import annotations
 
@@ -20,6 +26,22 @@ import torch
 import torch.nn as nn
 
 from . import _capi
+
+
+class BCELoss(nn.BCELoss):
+    """nn.BCELoss (model.py:21) that raises like the reference's CPU BCELoss ("all elements of
+    input should be between 0 and 1") when a prediction is NaN or outside [0, 1] -- e.g. the NaN
+    row of a single-item history equal to its target (model.py:92-95) -- instead of reaching the
+    ROCm kernel's device-side assert, which aborts the process. The check costs one device->host
+    sync; `check_input = False` skips it when the caller guarantees finite predictions."""
+
+    check_input = True
+
+    def forward(self, input, target):
+        if self.check_input and input.is_cuda and \
+                bool(((input < 0) | (input > 1) | torch.isnan(input)).any()):
+            raise RuntimeError("all elements of input should be between 0 and 1")
+        return super().forward(input, target)
 
 
 class _NAISDevice(nn.Module):
@@ -76,9 +98,11 @@ class _NAISDevice(nn.Module):
     def _run_forward(self, history, target, history_region=None, target_region=None,
                      target_lat_long=None, sigmoid=True):
         if self.training:
-            raise NotImplementedError(
-                f"{type(self).__name__}: training-mode forward (dropout + backward, SURVEY.md 8(f1)) "
-                "is not implemented on the HIP path yet; call model.eval()")
+            if not isinstance(self, NAIS_basic) or not sigmoid:
+                raise NotImplementedError(
+                    f"{type(self).__name__}: training-mode {'forward' if sigmoid else 'attention_network'}"
+                    " is implemented for NAIS_basic.forward only (SURVEY.md 8(f1)); call model.eval()")
+            return self._train_forward(history, target)
         dev = self._check_device(history, target, history_region, target_region, target_lat_long)
         if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
             raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
@@ -124,12 +148,105 @@ class _NAISDevice(nn.Module):
                 print(c)
         return out
 
+    # check that every row of a training batch carries the same history (batches.py:30); set to
+    # False to skip the check (one device->host sync per step) when the caller guarantees it
+    check_shared_history = True
+
+    def _train_forward(self, history, target):
+        dev = self._check_device(history, target)
+        if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
+            raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
+                             f"{tuple(target.shape)}")
+        history = history.to(torch.int64)
+        target = target.to(torch.int64).contiguous()
+        b, n = history.shape
+        if self.check_shared_history and b > 1 and n > 0 and \
+                not bool((history == history[:1]).all()):
+            raise NotImplementedError(
+                f"{type(self).__name__}: the training step needs rows that share one history "
+                "(get_NAIS_batch, batches.py:24-50); per-row histories are not supported")
+        hist = history[0].contiguous() if b > 0 else history.new_empty(0)
+        p = float(self.drop.p) if self.drop.training else 0.0
+        seed = int(torch.randint(0, 2**62, (1,)).item())   # torch's CPU generator: manual_seed applies
+        w = [self.embed_history.weight, self.embed_target.weight, self.attn_layer1.weight,
+             self.attn_layer1.bias, self.attn_layer2.weight]
+        pred, nan = _NAISTrainStep.apply(self, hist, target, p, seed, *w)
+        self._last_nan = nan
+        if self.report_nan:
+            c = int(nan.item())                              # model.py:50-54
+            if c > 0:
+                print(c)
+        return pred
+
     def get_mask(self, user_history, target_item):            # model.py:92-95
         target_item = target_item.reshape([len(target_item), 1])
         return user_history != target_item
 
     def loss_function(self, prediction, label):              # model.py:96-97
         return self.loss_func(prediction, label)
+
+
+class _NAISTrainStep(torch.autograd.Function):
+    """pred = sigmoid(attention_network(...)) of a shared-history batch with dropout; backward
+    through nais_train_backward (gradients of the five NAIS_basic parameters)."""
+
+    @staticmethod
+    def forward(ctx, module, hist, target, p, seed, eh, et, w1, b1, w2):
+        dev = eh.device
+        b, n = target.shape[0], hist.shape[0]
+        lib = _capi.load()
+        prm = module.nais_params()
+        pred = torch.empty(b, dtype=torch.float32, device=dev)
+        saved = torch.empty(2 * max(b, 1), dtype=torch.float32, device=dev)
+        nan = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws_bytes = lib.nais_train_workspace_size(prm, b, n)
+        ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
+        _capi.check(lib.nais_train_forward(prm, _capi.ptr(hist) if n else None, n,
+                                           _capi.ptr(target) if b else None, b, p, seed,
+                                           pred.data_ptr(), saved.data_ptr(), nan.data_ptr(),
+                                           ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
+                    "nais_train_forward")
+        ctx.module, ctx.p, ctx.seed = module, p, seed
+        ctx.save_for_backward(hist, target, pred, saved)
+        ctx.mark_non_differentiable(nan)
+        return pred, nan
+
+    @staticmethod
+    def backward(ctx, gpred, _gnan):
+        hist, target, pred, saved = ctx.saved_tensors
+        m = ctx.module
+        eh, et = m.embed_history.weight, m.embed_target.weight
+        w1, b1, w2 = m.attn_layer1.weight, m.attn_layer1.bias, m.attn_layer2.weight
+        g = [torch.zeros_like(t) for t in (eh, et, w1, b1, w2)]
+        b, n = target.shape[0], hist.shape[0]
+        gpred = gpred.to(torch.float32).contiguous()
+        lib = _capi.load()
+        _capi.check(lib.nais_train_backward(m.nais_params(), _capi.ptr(hist) if n else None, n,
+                                            _capi.ptr(target) if b else None, b, ctx.p, ctx.seed,
+                                            pred.data_ptr(), saved.data_ptr(), gpred.data_ptr(),
+                                            *[t.data_ptr() for t in g],
+                                            _capi.stream_handle(eh.device)),
+                    "nais_train_backward")
+        # rows of the embedding tables this step can have touched (for optim.Adagrad's row update)
+        _note_rows(eh, hist)
+        _note_rows(et, target)
+        return (None, None, None, None, None, *g)
+
+
+def _note_rows(param, rows):
+    """Record rows whose gradient this backward wrote; consumed (reset) by optim.Adagrad.step.
+    Without such a consumer (e.g. torch.optim.Adagrad) the record degrades to "dense" after a few
+    backward calls instead of growing."""
+    lst = getattr(param, "_nais_rows", None)
+    if isinstance(lst, str):
+        return
+    if lst is None:
+        lst = []
+        param._nais_rows = lst
+    if len(lst) >= 16:
+        param._nais_rows = "dense"
+        return
+    lst.append(rows)
 
 
 class NAIS_basic(_NAISDevice):
@@ -145,7 +262,7 @@ class NAIS_basic(_NAISDevice):
         self.embed_target = nn.Embedding(item_num, self.embed_size)
         self.relu = nn.ReLU()
         self.sigmoid = nn.Sigmoid()
-        self.loss_func = nn.BCELoss()
+        self.loss_func = BCELoss()
         self.drop = nn.Dropout()
         self.attn_layer1 = nn.Linear(self.embed_size, self.hidden_size)
         self.attn_layer2 = nn.Linear(self.hidden_size, 1, bias=False)
@@ -179,7 +296,7 @@ class NAIS_regionEmbedding(_NAISDevice):
         self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
         self.relu = nn.ReLU()
         self.sigmoid = nn.Sigmoid()
-        self.loss_func = nn.BCELoss()
+        self.loss_func = BCELoss()
         self.attn_layer1 = nn.Linear(embed_size, hidden_size)
         self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
         self.drop = nn.Dropout()
@@ -218,7 +335,7 @@ class NAIS_region_distance_Embedding(_NAISDevice):
         self.relu = nn.ReLU()
         self.tanh = nn.Tanh()
         self.sigmoid = nn.Sigmoid()
-        self.loss_func = nn.BCELoss()
+        self.loss_func = BCELoss()
         self.attn_layer1 = nn.Linear(embed_size + 2, hidden_size)
         self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
         self.dist_layer = nn.Linear(2, 2)

@@ -1,0 +1,247 @@
+"""GPU parity of the NAIS_basic training step through the C-ABI.
+
+* golden: the reference's own autograd gradients (tests/golden/train_step.npz, dropout off)
+* oracle: float64 restatement of forward + backward (oracle/train_oracle.py) on seeded
+  get_NAIS_batch-shaped batches (batches.py:24-50), with dropout p = 0.5 injected as the device's
+  own mask (nais_dropout_mask) so both sides drop the same units
+* Adagrad: nais_adagrad / nais_adagrad_rows against torch.optim.Adagrad's update (run.py:89)
+
+Tolerance: predictions within 1e-4 (SCORE_ATOL, the north star's fp32 bar); every gradient within
+GRAD_RTOL x max|reference gradient| of that tensor (fp32 MFMA + atomic summation order against a
+float64 / CPU-fp32 reference; observed ~1e-6).
+"""
+import numpy as np
+import pytest
+import torch
+
+from _helpers import SCORE_ATOL, load_golden
+from oracle import train_oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+GRAD_RTOL = 1e-4
+NAMES = ["embed_history.weight", "embed_target.weight", "attn_layer1.weight", "attn_layer1.bias",
+         "attn_layer2.weight"]
+
+
+def _model(p, beta=0.5, drop_p=0.0):
+    from poi_recommendation_models_amd import model as M
+    P, D = p["embed_history.weight"].shape
+    H = p["attn_layer1.weight"].shape[0]
+    m = M.NAIS_basic(P, D, H, beta)
+    sd = m.state_dict()
+    for k in sd:
+        sd[k] = torch.from_numpy(np.ascontiguousarray(p[k]))
+    m.load_state_dict(sd)
+    m.report_nan = False
+    m.drop.p = drop_p
+    return m.to(DEV).train()
+
+
+def _params(P, D, H, seed, emb_std=0.3):
+    r = np.random.default_rng(seed)
+    f = np.float32
+    bound = 1 / np.sqrt(D)
+    return {"embed_history.weight": r.normal(0, emb_std, (P, D)).astype(f),
+            "embed_target.weight": r.normal(0, emb_std, (P, D)).astype(f),
+            "attn_layer1.weight": r.uniform(-bound, bound, (H, D)).astype(f),
+            "attn_layer1.bias": r.normal(0, 0.1, H).astype(f),
+            "attn_layer2.weight": r.uniform(-1 / np.sqrt(H), 1 / np.sqrt(H), (1, H)).astype(f)}
+
+
+def _batch(P, n, num_ng, seed):
+    """get_NAIS_batch (batches.py:24-50): n positives (shuffled) shared as history by
+    n * (1 + num_ng) rows [pos, neg x num_ng] per positive, labels 1 / 0."""
+    r = np.random.default_rng(seed)
+    pos = r.choice(P, n, replace=False)
+    neg = r.choice(np.setdiff1d(np.arange(P), pos), n * num_ng, replace=False).reshape(n, num_ng)
+    data = np.concatenate([pos.reshape(-1, 1), neg], 1).reshape(-1)
+    labels = np.concatenate([np.ones((n, 1)), np.zeros((n, num_ng))], 1).reshape(-1).astype(np.float32)
+    hist = np.repeat(pos.reshape(1, -1), len(data), 0)
+    return hist, data, labels
+
+
+def _step(m, hist, data, labels):
+    for q in m.parameters():
+        q.grad = None
+    pred = m(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV))
+    loss = m.loss_func(pred, torch.as_tensor(labels).to(DEV))
+    loss.backward()
+    grads = {k: q.grad.detach().cpu().numpy() for k, q in m.named_parameters()}
+    return pred.detach().cpu().numpy(), float(loss.item()), grads
+
+
+def _assert_grads(got, ref, rtol=GRAD_RTOL):
+    worst = 0.0
+    for k in NAMES:
+        r = np.asarray(ref[k], np.float64).reshape(got[k].shape)
+        scale = max(np.abs(r).max(), 1e-30)
+        err = np.abs(got[k] - r).max() / scale
+        worst = max(worst, err)
+        assert err <= rtol, (k, err)
+    return worst
+
+
+def test_train_step_golden():
+    z = load_golden("train_step.npz")
+    p = {k[2:]: z[k] for k in z.files if k.startswith("p/")}
+    m = _model(p)
+    pred, loss, grads = _step(m, z["hist"], z["data"], z["labels"])
+    assert np.max(np.abs(pred - z["pred"])) <= SCORE_ATOL
+    assert abs(loss - float(z["loss"])) <= 1e-5
+    _assert_grads(grads, {k: z["grad/" + k] for k in NAMES})
+
+
+@pytest.mark.parametrize("D,H", [(8, 8), (16, 16), (32, 20), (32, 48), (64, 64)])
+@pytest.mark.parametrize("n", [1, 3, 37, 204])
+def test_train_step_oracle_shapes(D, H, n):
+    P = 3000
+    p = _params(P, D, H, seed=D * 1000 + H + n)
+    hist, data, labels = _batch(P, n, 4, seed=n)
+    m = _model(p)
+    ref = train_oracle.train_step_basic(p, hist, data, labels)
+    if n == 1:
+        # row 0's target is the whole history: S = 0 -> NaN (model.py:92-95), as the reference;
+        # BCELoss then raises (as the reference's CPU BCELoss does) instead of a device assert
+        pred = m(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV))
+        got = pred.detach().cpu().numpy()
+        assert np.isnan(got[0]) and np.isnan(ref["pred"][0])
+        assert np.array_equal(np.isnan(got), np.isnan(ref["pred"]))
+        assert np.max(np.abs(got[1:] - ref["pred"][1:])) <= SCORE_ATOL
+        with pytest.raises(RuntimeError, match="between 0 and 1"):
+            m.loss_func(pred, torch.as_tensor(labels).to(DEV))
+        return
+    pred, loss, grads = _step(m, hist, data, labels)
+    assert np.max(np.abs(pred - ref["pred"])) <= SCORE_ATOL
+    assert abs(loss - ref["loss"]) <= 1e-5
+    _assert_grads(grads, ref["grads"])
+
+
+def _mask(seed, b, n, H, p):
+    from poi_recommendation_models_amd import _capi
+    out = torch.empty(b * n * H, dtype=torch.uint8, device=DEV)
+    _capi.check(_capi.load().nais_dropout_mask(seed, b, n, H, p, out.data_ptr(),
+                                               _capi.stream_handle(torch.device(DEV))),
+                "nais_dropout_mask")
+    return out.view(b, n, H).cpu().numpy()
+
+
+def test_dropout_mask_statistics():
+    m = _mask(1234, 1020, 204, 64, 0.5)
+    assert abs(m.mean() - 0.5) < 2e-3
+    assert np.array_equal(m, _mask(1234, 1020, 204, 64, 0.5))           # deterministic per seed
+    assert (m != _mask(1235, 1020, 204, 64, 0.5)).mean() > 0.45         # new seed, new mask
+    assert _mask(7, 4, 3, 16, 0.0).all() and not _mask(7, 4, 3, 16, 1.0).any()
+    assert abs(_mask(9, 256, 64, 64, 0.2).mean() - 0.8) < 3e-3
+
+
+@pytest.mark.parametrize("D,H,n", [(16, 16, 12), (64, 64, 204)])
+def test_train_step_dropout_injected(D, H, n, monkeypatch):
+    """Dropout on: the oracle applies the device's mask for the same seed."""
+    P = 5000
+    p = _params(P, D, H, seed=n)
+    hist, data, labels = _batch(P, n, 4, seed=n + 1)
+    m = _model(p, drop_p=0.5)
+    seed = 987654321
+    monkeypatch.setattr(torch, "randint", lambda *a, **k: torch.tensor([seed]))
+    pred, loss, grads = _step(m, hist, data, labels)
+    keep = _mask(seed, len(data), n, H, 0.5)
+    ref = train_oracle.train_step_basic(p, hist, data, labels, keep=keep, drop_p=0.5)
+    assert np.max(np.abs(pred - ref["pred"])) <= SCORE_ATOL
+    assert abs(loss - ref["loss"]) <= 1e-5
+    _assert_grads(grads, ref["grads"])
+
+
+def test_train_empty_history():
+    P, D, H = 100, 16, 16
+    m = _model(_params(P, D, H, 3))
+    pred, loss, grads = _step(m, np.zeros((5, 0), np.int64), np.arange(5), np.ones(5, np.float32))
+    assert np.all(pred == 0.5)
+    for k in NAMES:
+        assert not np.any(grads[k])
+
+
+def test_train_per_row_history_raises():
+    m = _model(_params(100, 16, 16, 4))
+    hist = np.array([[1, 2], [3, 4]])
+    with pytest.raises(NotImplementedError):
+        m(torch.as_tensor(hist).to(DEV), torch.as_tensor([5, 6]).to(DEV))
+
+
+@pytest.mark.parametrize("wd,lr_decay", [(0.0, 0.0), (0.01, 0.0), (0.0, 0.1)])
+def test_adagrad_matches_torch(wd, lr_decay):
+    from poi_recommendation_models_amd import optim
+    torch.manual_seed(0)
+    shapes = [(3000, 64), (64, 64), (64,), (1, 64)]
+    ps = [torch.randn(s) for s in shapes]
+    ours = [torch.nn.Parameter(x.clone().to(DEV)) for x in ps]
+    ref = [torch.nn.Parameter(x.clone()) for x in ps]
+    o = optim.Adagrad(ours, lr=0.05, lr_decay=lr_decay, weight_decay=wd)
+    r = torch.optim.Adagrad(ref, lr=0.05, lr_decay=lr_decay, weight_decay=wd, foreach=False)
+    for step in range(3):
+        gs = [torch.randn(s) for s in shapes]
+        for q, g in zip(ours, gs):
+            q.grad = g.to(DEV)
+        for q, g in zip(ref, gs):
+            q.grad = g.clone()
+        o.step()
+        r.step()
+    for a, b in zip(ours, ref):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().numpy(), rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(o.state[a]["sum"].cpu().numpy(), r.state[b]["sum"].numpy(),
+                                   rtol=1e-6, atol=1e-7)
+
+
+def test_adagrad_rows_bit_identical_to_dense():
+    """Row update == dense update bit for bit when the gradient is zero outside the rows (the
+    embedding grads of a training backward: rows = the batch's history / targets)."""
+    from poi_recommendation_models_amd import optim
+    P, D, H, n = 4000, 64, 64, 50
+    p = _params(P, D, H, 11)
+    hist, data, labels = _batch(P, n, 4, seed=5)
+    m = _model(p)
+    _, _, grads = _step(m, hist, data, labels)      # one set of gradients for both optimizers
+    pa = [torch.nn.Parameter(q.detach().clone()) for q in m.parameters()]
+    pb = [torch.nn.Parameter(q.detach().clone()) for q in m.parameters()]
+    oa = optim.Adagrad(pa, lr=0.01)
+    ob = optim.Adagrad(pb, lr=0.01, row_update=False)
+    rows = {0: torch.as_tensor(hist[0]).to(DEV), 1: torch.as_tensor(data).to(DEV)}
+    for _ in range(3):
+        for i, (qa, qb, k) in enumerate(zip(pa, pb, NAMES)):
+            g = torch.as_tensor(grads[k]).to(DEV)
+            qa.grad, qb.grad = g.clone(), g.clone()
+            if i in rows:
+                qa._nais_rows = [rows[i]]
+        oa.step()
+        ob.step()
+    for qa, qb, k in zip(pa, pb, NAMES):
+        assert torch.equal(qa, qb), k
+        assert torch.equal(oa.state[qa]["sum"], ob.state[qb]["sum"]), k
+
+
+def test_training_loop_matches_oracle():
+    """Three run.py-style steps (forward, BCELoss, backward, Adagrad) against the oracle."""
+    from poi_recommendation_models_amd import optim
+    P, D, H, n = 2000, 32, 32, 40
+    p = _params(P, D, H, 21)
+    m = _model(p)
+    o = optim.Adagrad(m.parameters(), lr=0.01)
+    ref = {k: v.copy() for k, v in p.items()}
+    st = {k: np.zeros_like(v) for k, v in p.items()}
+    for step in range(1, 4):
+        hist, data, labels = _batch(P, n, 4, seed=100 + step)
+        o.zero_grad()
+        pred, loss, _ = _step(m, hist, data, labels)
+        o.step()
+        r = train_oracle.train_step_basic(ref, hist, data, labels)
+        assert abs(loss - r["loss"]) <= 1e-5
+        for k in NAMES:
+            ref[k], st[k] = train_oracle.adagrad(ref[k], st[k], r["grads"][k].reshape(ref[k].shape),
+                                                 0.01, step)
+    # Adagrad's first steps divide by |g|: an element whose true gradient is ~1e-6 of the tensor's
+    # largest can flip sign under fp32 rounding and move by 2 lr, so a tiny fraction may differ.
+    for k, q in m.named_parameters():
+        got = q.detach().cpu().numpy()
+        bad = ~np.isclose(got, ref[k], rtol=1e-4, atol=2e-5)
+        assert bad.mean() <= 1e-3, (k, int(bad.sum()), bad.size)

@@ -105,3 +105,33 @@ def test_powerlaw_dist_prd_predict():
     np.testing.assert_array_equal(norm, z["normalize"])
     assert powerlaw_oracle.normalize([0.0, 0.0, 0.0]) == list(z["normalize_zero"])
     assert not any(math.isnan(x) for x in d)
+
+
+def test_train_oracle_golden():
+    """Training-step restatement (oracle/train_oracle.py) against the reference's own autograd
+    gradients (run.py:101-105 on a get_NAIS_batch batch, dropout off)."""
+    from oracle import train_oracle
+    z = load_golden("train_step.npz")
+    p = {k[2:]: z[k] for k in z.files if k.startswith("p/")}
+    r = train_oracle.train_step_basic(p, z["hist"], z["data"], z["labels"])
+    assert np.max(np.abs(r["pred"] - z["pred"])) <= 1e-6
+    assert abs(r["loss"] - float(z["loss"])) <= 1e-6
+    for k, g in r["grads"].items():
+        ref = z["grad/" + k]
+        assert np.max(np.abs(g.reshape(ref.shape) - ref)) <= 1e-6 * np.abs(ref).max(), k
+
+
+def test_train_oracle_adagrad_matches_torch():
+    import torch
+    from oracle import train_oracle
+    rng = np.random.default_rng(0)
+    p0 = rng.normal(size=(50, 8)).astype(np.float32)
+    q = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+    opt = torch.optim.Adagrad([q], lr=0.05, lr_decay=0.1, weight_decay=0.01, foreach=False)
+    p, st = p0.copy(), np.zeros_like(p0)
+    for step in range(1, 4):
+        g = rng.normal(size=p0.shape).astype(np.float32)
+        q.grad = torch.from_numpy(g.copy())
+        opt.step()
+        p, st = train_oracle.adagrad(p, st, g, 0.05, step, lr_decay=0.1, weight_decay=0.01)
+    np.testing.assert_allclose(p, q.detach().numpy(), rtol=1e-6, atol=1e-7)
