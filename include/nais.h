@@ -207,8 +207,10 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *   backward; optional nan_count (+= rows whose logit is NaN, model.py:50-54).
  * nais_train_backward: given grad_pred[b] = dL/dpred (e.g. from BCELoss's backward), ADDS the
  *   gradients into grad_embed_history / grad_embed_target ([num_pois, embed_dim], dense, rows by
- *   POI id), grad_w1 [hidden, embed_dim], grad_b1 [hidden], grad_w2 [hidden] (fp32 atomics: the
- *   summation order is not fixed). Same params, hist, target, dropout_p and seed as the forward.
+ *   POI id; repeated ids are summed with fp32 atomics), grad_w1 [hidden, embed_dim], grad_b1
+ *   [hidden], grad_w2 [hidden]. Same params, hist, target, dropout_p and seed as the forward.
+ *   Both calls take a workspace of nais_train_workspace_size(params, b, n) bytes (the forward's
+ *   may be reused by the backward once the forward has run).
  * -------------------------------------------------------------------------------------------- */
 size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n);
 
@@ -221,7 +223,8 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
                             const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
                             const float* pred, const float* saved, const float* grad_pred,
                             float* grad_embed_history, float* grad_embed_target, float* grad_w1,
-                            float* grad_b1, float* grad_w2, void* stream);
+                            float* grad_b1, float* grad_w2, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
                           uint8_t* out, void* stream);

@@ -96,7 +96,7 @@ def load(path: str | None = None):
                                        vp, vp, sz, vp]
     lib.nais_train_backward.restype = i32
     lib.nais_train_backward.argtypes = [ctypes.POINTER(NaisParams), vp, i64, vp, i64, f32, u64, vp, vp,
-                                        vp, vp, vp, vp, vp, vp, vp]
+                                        vp, vp, vp, vp, vp, vp, vp, sz, vp]
     lib.nais_dropout_mask.restype = i32
     lib.nais_dropout_mask.argtypes = [u64, i64, i64, i32, f32, vp, vp]
     lib.nais_adagrad.restype = i32

@@ -20,21 +20,25 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build(force=False, extra=()):
+def build(force=False, extra=(), out=None):
+    """Compile the kernels into OUT (or `out`, e.g. an A/B variant with extra -D flags)."""
+    if out is not None:
+        force = True
+    OUT_ = out or OUT
     deps = [*SRCS, os.path.join(HERE, "csrc", "nais_internal.h"), os.path.join(ROOT, "include", "nais.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
+    if not force and os.path.exists(OUT_) and all(os.path.getmtime(OUT_) >= os.path.getmtime(d) for d in deps):
+        return OUT_
     # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds/muls into v_pk_*_f32, which
     # cost more issue slots than two scalar ops beside MFMAs (cdna_hip_programming.md, price table);
     # measured +5 % on the split-fp16 catalog kernel (profiles/r1/ab_*.json).
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", *SRCS, *extra]
+           "-I", os.path.join(ROOT, "include"), "-o", OUT_ + ".tmp", *SRCS, *extra]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc failed ({r.returncode}): {' '.join(cmd)}")
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(OUT_ + ".tmp", OUT_)
+    return OUT_
 
 
 if __name__ == "__main__":

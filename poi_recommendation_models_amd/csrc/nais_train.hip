@@ -47,6 +47,31 @@ constexpr int TTHREADS = TW * 64;
 constexpr int TROWS = TW * 32;      // batch rows per workgroup: 32 per wave (the MFMA columns)
 constexpr int MAX_JS = 32;          // history items per slice (grid.y)
 
+// Optional per-phase cycle accounting of the backward kernel (A/B builds only:
+// -DNAIS_TRAIN_TIMING=1 adds nais_debug_train_cycles(); scripts/train_phases.py reads it).
+#ifndef NAIS_TRAIN_TIMING
+#define NAIS_TRAIN_TIMING 0
+#endif
+#if NAIS_TRAIN_TIMING
+__device__ unsigned long long g_train_cycles[16];
+#define TSTART() unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[16] = {0}
+#define TMARK(k)                                            \
+  do {                                                      \
+    const unsigned long long t_now = __builtin_amdgcn_s_memtime(); \
+    t_acc[k] += t_now - t_prev;                             \
+    t_prev = t_now;                                         \
+  } while (0)
+#define TFLUSH()                                                             \
+  do {                                                                       \
+    if ((threadIdx.x & 63) == 0)                                             \
+      for (int q = 0; q < 16; ++q) atomicAdd(&g_train_cycles[q], t_acc[q]);  \
+  } while (0)
+#else
+#define TSTART() (void)0
+#define TMARK(k) (void)0
+#define TFLUSH() (void)0
+#endif
+
 __device__ __forceinline__ floatx16 mfma(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -132,7 +157,8 @@ struct TL {
   static constexpr int O_DH = O_W1T + DW * W1TP;    // dh accumulator [MAX_JS][D]
   static constexpr int O_X = O_DH + MAX_JS * D;     // x of the workgroup's rows [TROWS][XP]
   static constexpr int O_U = O_X + TROWS * XP;      // du of the workgroup's rows [TROWS][UP]
-  static constexpr int BWD = O_U + TROWS * UP;
+  static constexpr int O_BW = O_U + TROWS * UP;     // db1 | dw2 of the workgroup [2][HW]
+  static constexpr int BWD = O_BW + 2 * HW;
 };
 
 template <int DH, int HB>
@@ -324,9 +350,9 @@ __global__ void train_finalize_kernel(const float* __restrict__ Sp, const float*
 template <int DH, int HB>
 __global__ void __launch_bounds__(TTHREADS, 1)
 train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
-                      const float* __restrict__ gpred, float* __restrict__ g_eh,
-                      float* __restrict__ g_et, float* __restrict__ g_w1, float* __restrict__ g_b1,
-                      float* __restrict__ g_w2) {
+                      const float* __restrict__ gpred, float* __restrict__ Wt,
+                      float* __restrict__ Ww, float* __restrict__ Wh) {
+  TSTART();
   using T = TL<DH, HB>;
   constexpr int D = T::D;
   constexpr int DB = (DH + 15) / 16;             // 32-dim blocks of dx / dW1 columns
@@ -346,6 +372,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
   stage_w<DH, HB>(a, L, tid, true);
   stage_hist<DH, HB>(a, L, tid, j0, nj);
   for (int f = tid; f < MAX_JS * D; f += TTHREADS) L[T::O_DH + f] = 0.f;
+  for (int f = tid; f < 2 * T::HW; f += TTHREADS) L[T::O_BW + f] = 0.f;
   for (int f = tid; f < TROWS * T::XP; f += TTHREADS) L[T::O_X + f] = 0.f;  // dims >= D stay 0
   float t[DH];
   load_target<DH>(a, tgt, active, hh, t);
@@ -373,6 +400,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
     for (int r = 0; r < 16; ++r) gw[tt][r] = 0.f;
   __syncthreads();
 
+  TMARK(0);
   float* xrow = L + T::O_X + (w * 32 + ci) * T::XP;
   float* urow = L + T::O_U + (w * 32 + ci) * T::UP;
   for (int jj = 0; jj < nj; ++jj) {
@@ -381,6 +409,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
     pair_forward<DH, HB>(a, L, L + T::O_H + jj * D, t, lane, uint32_t(c * a.n + j0 + jj), h, x,
                          acc, sdot, at);
     const float e = expf(at) * (a.hist[j0 + jj] != tgt ? 1.f : 0.f);
+    TMARK(1);
     const float ds = gl * e;
     const float da = ds * (sdot - bns);
 #pragma unroll
@@ -408,6 +437,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
         *reinterpret_cast<float4*>(urow + 32 * hb + 8 * g + 4 * hh) =
             make_float4(acc[hb][4 * g], acc[hb][4 * g + 1], acc[hb][4 * g + 2], acc[hb][4 * g + 3]);
 
+    TMARK(2);
     // dx = W1^T du, du taken from the accumulator registers as the B operand
     floatx16 dx[DB];
 #pragma unroll
@@ -433,9 +463,12 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
       dt[s] = fmaf(r, h[s], dt[s]);
       vh[s] = r * t[s];
     }
+    TMARK(3);
     const float hsum = half_reduce_scatter<DH>(vh, lane);
     if ((ci & ((1 << SHD) - 1)) == 0) atomicAdd(&L[T::O_DH + jj * D + kdim(ci >> SHD, hh)], hsum);
+    TMARK(4);
     __syncthreads();
+    TMARK(5);
     // dW1 tiles: A = du^T rows (hidden), B = x rows (dims), K over the 128 rows
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
@@ -451,10 +484,16 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
         }
       }
     }
+    TMARK(6);
     __syncthreads();
+    TMARK(7);
   }
 
-  // ---- flush: dW1, db1, dw2, dt (per row), dh (per history item)
+  // ---- partials of this workgroup (plain stores; train_reduce_kernel sums them):
+  //   Wt [slices][b][D] dt per row, Ww [workgroups][H*D + 2H] dW1 | db1 | dw2,
+  //   Wh [row blocks][n][D] dh per history item
+  const int64_t blk = int64_t(blockIdx.y) * gridDim.x + blockIdx.x;
+  const int wsz = a.H * D + 2 * a.H;
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt) {
     const int tile = w + TW * tt;
@@ -464,7 +503,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = crow(ib, r, hh);
-        if (row < a.H && col < D) unsafeAtomicAdd(&g_w1[row * D + col], gw[tt][r]);
+        if (row < a.H && col < D) Ww[blk * wsz + row * D + col] = gw[tt][r];
       }
     }
   }
@@ -474,19 +513,64 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
     if ((ci & ((1 << SHH) - 1)) == 0) {
       const int m = ci >> SHH;
       const int i = crow(m >> 4, m & 15, hh);
-      if (i < a.H) {
-        unsafeAtomicAdd(&g_b1[i], sb);
-        unsafeAtomicAdd(&g_w2[i], sw);
-      }
+      atomicAdd(&L[T::O_BW + i], sb);
+      atomicAdd(&L[T::O_BW + T::HW + i], sw);
     }
   }
   if (active) {
+    float* dst = Wt + (int64_t(blockIdx.y) * a.b + c) * D;
 #pragma unroll
-    for (int s = 0; s < DH; ++s) unsafeAtomicAdd(&g_et[tgt * D + kdim(s, hh)], dt[s]);
+    for (int g = 0; g < DH / 4; ++g)
+      *reinterpret_cast<float4*>(dst + kdim4(g, hh)) =
+          make_float4(dt[4 * g], dt[4 * g + 1], dt[4 * g + 2], dt[4 * g + 3]);
   }
   __syncthreads();
+  for (int i = tid; i < a.H; i += TTHREADS) {
+    Ww[blk * wsz + a.H * D + i] = L[T::O_BW + i];
+    Ww[blk * wsz + a.H * D + a.H + i] = L[T::O_BW + T::HW + i];
+  }
   for (int f = tid; f < nj * D; f += TTHREADS)
-    unsafeAtomicAdd(&g_eh[a.hist[j0 + f / D] * D + f % D], L[T::O_DH + f]);
+    Wh[(int64_t(blockIdx.x) * a.n + j0) * D + f] = L[T::O_DH + f];
+  TMARK(8);
+  TFLUSH();
+}
+
+constexpr int REDUCE_KS = 16;
+
+// Sums the backward partials into the caller's gradients (+=): dW1 | db1 | dw2 over workgroups,
+// dt over slices scattered to embed_target rows, dh over row blocks scattered to embed_history
+// rows (atomics only for the two scatters, where POI ids may repeat).
+__global__ void train_reduce_kernel(const float* __restrict__ Wt, const float* __restrict__ Ww,
+                                    const float* __restrict__ Wh, int64_t b, int64_t n, int D,
+                                    int H, int ns, int rb, const int64_t* __restrict__ hist,
+                                    const int64_t* __restrict__ target, float* g_eh, float* g_et,
+                                    float* g_w1, float* g_b1, float* g_w2) {
+  const int64_t wsz = int64_t(H) * D + 2 * H;
+  const int64_t nblk = int64_t(ns) * rb;
+  const int64_t nw = wsz * REDUCE_KS, nt = b * D, nh = n * D;
+  const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e < nw) {  // REDUCE_KS threads per weight, each over every REDUCE_KS-th workgroup
+    const int64_t el = e % wsz, part = e / wsz;
+    float sum = 0.f;
+#pragma unroll 4
+    for (int64_t k = part; k < nblk; k += REDUCE_KS) sum += Ww[k * wsz + el];
+    float* dst = el < int64_t(H) * D ? g_w1 + el
+               : el < int64_t(H) * D + H ? g_b1 + (el - int64_t(H) * D)
+                                         : g_w2 + (el - int64_t(H) * D - H);
+    unsafeAtomicAdd(dst, sum);
+  } else if (e < nw + nt) {
+    const int64_t f = e - nw, c = f / D, d = f % D;
+    float sum = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) sum += Wt[(int64_t(k) * b + c) * D + d];
+    unsafeAtomicAdd(&g_et[target[c] * D + d], sum);
+  } else if (e < nw + nt + nh) {
+    const int64_t f = e - nw - nt, j = f / D, d = f % D;
+    float sum = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < rb; ++k) sum += Wh[(int64_t(k) * n + j) * D + d];
+    unsafeAtomicAdd(&g_eh[hist[j] * D + d], sum);
+  }
 }
 
 __global__ void dropout_mask_kernel(Drop d, int64_t b, int64_t n, int H, uint8_t* out) {
@@ -583,7 +667,7 @@ int slice_items(int64_t b, int64_t n, int per_cu) {
   int64_t js = (n * rb + want - 1) / want;
   return (int)std::max<int64_t>(1, std::min<int64_t>(MAX_JS, js));
 }
-constexpr int FWD_PER_CU = 4, BWD_PER_CU = 1;
+constexpr int FWD_PER_CU = 1, BWD_PER_CU = 1;
 
 template <typename K>
 void set_lds(K kern, size_t bytes) {
@@ -604,15 +688,13 @@ int launch_train_forward(const TrainArgs& a, float* Sp, float* Np, hipStream_t s
 
 template <int DH, int HB>
 int launch_train_backward(const TrainArgs& a, const float* saved, const float* pred,
-                          const float* gpred, float* g_eh, float* g_et, float* g_w1, float* g_b1,
-                          float* g_w2, hipStream_t st) {
+                          const float* gpred, float* Wt, float* Ww, float* Wh, hipStream_t st) {
   const size_t lds = size_t(TL<DH, HB>::BWD) * 4;
   auto kern = train_backward_kernel<DH, HB>;
   static bool once = (set_lds(kern, lds), true);
   (void)once;
   dim3 grid((unsigned)((a.b + TROWS - 1) / TROWS), (unsigned)((a.n + a.js - 1) / a.js));
-  hipLaunchKernelGGL(kern, grid, dim3(TTHREADS), lds, st, a, saved, pred, gpred, g_eh, g_et, g_w1,
-                     g_b1, g_w2);
+  hipLaunchKernelGGL(kern, grid, dim3(TTHREADS), lds, st, a, saved, pred, gpred, Wt, Ww, Wh);
   return nais_internal_check_launch("train_backward_kernel");
 }
 
@@ -646,11 +728,13 @@ int hip_rc(hipError_t e, const char* what) {
 extern "C" {
 
 size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
-  (void)params;
-  if (b <= 0 || n <= 0) return 0;
+  if (!params || b <= 0 || n <= 0) return 0;
   const int js = slice_items(b, n, FWD_PER_CU);
-  const int64_t ns = (n + js - 1) / js;
-  return size_t(2 * ns * b) * sizeof(float);
+  const int64_t ns = (n + js - 1) / js, rb = (b + TROWS - 1) / TROWS;
+  const int64_t D = params->embed_dim, H = params->hidden;
+  const int64_t fwd = 2 * ns * b;
+  const int64_t bwd = ns * b * D + ns * rb * (H * D + 2 * H) + rb * n * D;
+  return size_t(std::max(fwd, bwd)) * sizeof(float);
 }
 
 int32_t nais_train_forward(const nais_params_t* params, const int64_t* hist, int64_t n,
@@ -690,7 +774,8 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
                             const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
                             const float* pred, const float* saved, const float* grad_pred,
                             float* grad_embed_history, float* grad_embed_target, float* grad_w1,
-                            float* grad_b1, float* grad_w2, void* stream) {
+                            float* grad_b1, float* grad_w2, void* workspace,
+                            size_t workspace_bytes, void* stream) {
   TShape sh;
   int rc = tvalidate(params, &sh);
   if (rc) return rc;
@@ -702,13 +787,23 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
       !grad_b1 || !grad_w2)
     return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved/grad pointer");
   const int js = slice_items(b, n, BWD_PER_CU);
-  if ((n + js - 1) / js > 65535)
-    return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  const int64_t ns = (n + js - 1) / js, rb = (b + TROWS - 1) / TROWS;
+  if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  if (!workspace || workspace_bytes < nais_train_workspace_size(params, b, n))
+    return nais_internal_fail(NAIS_E_WORKSPACE, "workspace too small (nais_train_workspace_size)");
+  const int64_t D = params->embed_dim, H = params->hidden;
+  float* Wt = static_cast<float*>(workspace);
+  float* Ww = Wt + ns * b * D;
+  float* Wh = Ww + ns * rb * (H * D + 2 * H);
   const TrainArgs a = targs(params, hist, n, target, b, js, dropout_p, seed);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  NAIS_TRAIN_DISPATCH(launch_train_backward, sh, a, saved, pred, grad_pred, grad_embed_history,
-                      grad_embed_target, grad_w1, grad_b1, grad_w2, st);
-  return rc;
+  NAIS_TRAIN_DISPATCH(launch_train_backward, sh, a, saved, pred, grad_pred, Wt, Ww, Wh, st);
+  if (rc) return rc;
+  const int64_t total = (H * D + 2 * H) * REDUCE_KS + b * D + n * D;
+  hipLaunchKernelGGL(train_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     Wt, Ww, Wh, b, n, (int)D, (int)H, (int)ns, (int)rb, hist, target,
+                     grad_embed_history, grad_embed_target, grad_w1, grad_b1, grad_w2);
+  return nais_internal_check_launch("train_reduce_kernel");
 }
 
 int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
@@ -751,5 +846,18 @@ int32_t nais_adagrad_rows(float* param, float* state_sum, const float* grad, int
                      num_rows, clr, eps);
   return nais_internal_check_launch("adagrad_rows_kernel");
 }
+
+#if NAIS_TRAIN_TIMING
+int32_t nais_debug_train_cycles(unsigned long long* out16, int32_t reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_train_cycles), 16 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return NAIS_E_HIP;
+  if (reset) {
+    static const unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_train_cycles), z, sizeof(z)) != hipSuccess) return NAIS_E_HIP;
+  }
+  return NAIS_OK;
+}
+#endif
 
 }  // extern "C"

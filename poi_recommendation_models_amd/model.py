@@ -221,10 +221,13 @@ class _NAISTrainStep(torch.autograd.Function):
         b, n = target.shape[0], hist.shape[0]
         gpred = gpred.to(torch.float32).contiguous()
         lib = _capi.load()
-        _capi.check(lib.nais_train_backward(m.nais_params(), _capi.ptr(hist) if n else None, n,
+        prm = m.nais_params()
+        ws_bytes = lib.nais_train_workspace_size(prm, b, n)
+        ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=eh.device)
+        _capi.check(lib.nais_train_backward(prm, _capi.ptr(hist) if n else None, n,
                                             _capi.ptr(target) if b else None, b, ctx.p, ctx.seed,
                                             pred.data_ptr(), saved.data_ptr(), gpred.data_ptr(),
-                                            *[t.data_ptr() for t in g],
+                                            *[t.data_ptr() for t in g], ws.data_ptr(), ws_bytes,
                                             _capi.stream_handle(eh.device)),
                     "nais_train_backward")
         # rows of the embedding tables this step can have touched (for optim.Adagrad's row update)

@@ -145,7 +145,7 @@ def main():
     def bwd():
         _capi.check(lib.nais_train_backward(prm, hist1.data_ptr(), n, data1.data_ptr(), b, a.dropout, 7,
                                             pred.data_ptr(), saved.data_ptr(), gp.data_ptr(),
-                                            *[x.data_ptr() for x in g], sh), "bwd")
+                                            *[x.data_ptr() for x in g], ws.data_ptr(), ws_bytes, sh), "bwd")
     with torch.cuda.stream(st):
         for _ in range(3):
             fwd()
