@@ -229,6 +229,51 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
 int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
                           uint8_t* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Fused training step (run.py:101-109 in one call): forward, BCELoss (model.py:21) added into
+ * *loss_sum (device float, mean over the b rows -- run.py's train_loss accumulates loss.item()),
+ * backward, and torch.optim.Adagrad's update of all five parameters IN PLACE (the params pointers
+ * are written). Adagrad state lives in nais_adagrad_state_t; its gradient scratch must be all zero
+ * on entry and is left all zero. Rows with a NaN prediction (a single-item history equal to its
+ * target, model.py:92-95) are counted into *bad_rows (device int32); while *bad_rows != 0 the
+ * update is skipped (the reference's BCELoss raises on such a batch). pred [b] is optional.
+ * Workspace: nais_train_step_workspace_size(params, b, n) bytes.
+ * -------------------------------------------------------------------------------------------- */
+typedef struct nais_adagrad_state {
+  float lr, lr_decay, weight_decay, eps;   /* torch.optim.Adagrad arguments (run.py:89)            */
+  int64_t step;                            /* step count including this one (torch state['step']) */
+  float* sum_embed_history;                /* Adagrad accumulators, shapes of the parameters       */
+  float* sum_embed_target;
+  float* sum_w1;
+  float* sum_b1;
+  float* sum_w2;
+  float* grad_embed_history;               /* [P, D] zero-maintained gradient scratch              */
+  float* grad_embed_target;                /* [P, D]                                               */
+  float* grad_small;                       /* [H*D + 2H]: w1 | b1 | w2                             */
+  int32_t* stamp_embed_history;            /* [P] row-claim stamps, initialised to 0               */
+  int32_t* stamp_embed_target;             /* [P]                                                  */
+} nais_adagrad_state_t;
+
+size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, int64_t n);
+
+int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
+                        const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
+                        int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
+                        int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/*
+ * get_NAIS_batch (batches.py:24-50) for one user on the device: hist [n] = the
+ * user's n = indptr[user+1]-indptr[user] positives (CSR rows sorted ascending) in a seeded random
+ * order; target / labels [n * (1 + num_ng)] = rows [pos_i, neg_i1 .. neg_i,num_ng], labels 1 / 0.
+ * Negatives: distinct, uniform over the POIs not in the history (the reference's shuffle-and-slice
+ * distribution; not Python's random stream). *err (optional) is set to 1 if n disagrees with indptr.
+ */
+int32_t nais_make_train_batch(const int64_t* indptr, const int64_t* indices, int64_t user,
+                              int64_t n, int64_t num_pois, int32_t num_ng, uint64_t seed,
+                              int64_t* hist, int64_t* target, float* labels, int32_t* err,
+                              void* stream);
+
 /*
  * torch.optim.Adagrad's update (run.py:89; lr_decay folded into clr = lr / (1 + (step-1) lr_decay)):
  *   g' = g + weight_decay * p ; state += g' * g' ; p -= clr * g' / (sqrt(state) + eps)

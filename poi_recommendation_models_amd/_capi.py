@@ -21,7 +21,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_powerlaw_prior",
            "nais_distance_histogram", "nais_gather_rows", "nais_train_workspace_size",
            "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
-           "nais_adagrad_rows")
+           "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
+           "nais_make_train_batch")
 
 
 class NaisParams(ctypes.Structure):
@@ -41,6 +42,15 @@ class NaisPrior(ctypes.Structure):
     """Mirror of `nais_prior_t`."""
     _fields_ = [("a", ctypes.c_double), ("b", ctypes.c_double), ("alpha", ctypes.c_double),
                 ("coords", ctypes.c_void_p)]
+
+
+class NaisAdagradState(ctypes.Structure):
+    """Mirror of `nais_adagrad_state_t`."""
+    _fields_ = [("lr", ctypes.c_float), ("lr_decay", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("eps", ctypes.c_float), ("step", ctypes.c_int64)] + \
+        [(n, ctypes.c_void_p) for n in ("sum_embed_history", "sum_embed_target", "sum_w1", "sum_b1",
+                                        "sum_w2", "grad_embed_history", "grad_embed_target",
+                                        "grad_small", "stamp_embed_history", "stamp_embed_target")]
 
 
 class NaisError(RuntimeError):
@@ -103,6 +113,13 @@ def load(path: str | None = None):
     lib.nais_adagrad.argtypes = [vp, vp, vp, i64, f32, f32, f32, vp]
     lib.nais_adagrad_rows.restype = i32
     lib.nais_adagrad_rows.argtypes = [vp, vp, vp, i32, vp, i64, f32, f32, vp]
+    lib.nais_train_step_workspace_size.restype = sz
+    lib.nais_train_step_workspace_size.argtypes = [ctypes.POINTER(NaisParams), i64, i64]
+    lib.nais_train_step.restype = i32
+    lib.nais_train_step.argtypes = [ctypes.POINTER(NaisParams), ctypes.POINTER(NaisAdagradState), vp,
+                                    i64, vp, vp, i64, f32, u64, vp, vp, vp, vp, sz, vp]
+    lib.nais_make_train_batch.restype = i32
+    lib.nais_make_train_batch.argtypes = [vp, vp, i64, i64, i64, i32, u64, vp, vp, vp, vp, vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

@@ -23,6 +23,8 @@ class DeviceCSR:
 
     def __init__(self, train_matrix, device):
         X = train_matrix.tocsr() if not hasattr(train_matrix, "indptr") else train_matrix
+        if not X.has_sorted_indices:   # rows ascending (the batch builder binary-searches them)
+            X = X.sorted_indices()
         self.shape = X.shape
         self.host_indptr = np.asarray(X.indptr, dtype=np.int64)
         self.host_indices = np.asarray(X.indices, dtype=np.int64)

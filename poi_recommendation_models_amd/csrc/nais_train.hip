@@ -343,6 +343,44 @@ __global__ void train_finalize_kernel(const float* __restrict__ Sp, const float*
   if (nan_count && logit != logit) atomicAdd(nan_count, 1);
 }
 
+// Fused-step variant of the finalize: also the BCELoss of model.py:21 / run.py:104 (mean over the
+// b rows, log clamped at -100 as torch does) added into *loss_sum, and dL/dpred of its backward,
+// (p - y) / max((1 - p) p, 1e-12) / b. Rows whose prediction is NaN are counted in *bad_rows (the
+// reference's BCELoss raises on them); the update kernels then skip the step.
+__global__ void train_loss_kernel(const float* __restrict__ Sp, const float* __restrict__ Np,
+                                  int ns, int64_t b, int64_t n, float beta,
+                                  const float* __restrict__ labels, float* pred, float* saved,
+                                  float* gpred, float* loss_sum, int32_t* bad_rows) {
+  __shared__ float red[256 / 64];
+  const int64_t c = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  float term = 0.f;
+  if (c < b) {
+    float S = 0.f, N = 0.f;
+    for (int s = 0; s < ns; ++s) {
+      S += Sp[int64_t(s) * b + c];
+      N += Np[int64_t(s) * b + c];
+    }
+    float logit = 0.f;
+    if (n > 0) logit = N / ((beta == 0.5f) ? sqrtf(S) : powf(S, beta));
+    const float p = 1.0f / (1.0f + expf(-logit));
+    const float y = labels[c];
+    pred[c] = p;
+    saved[c] = S;
+    saved[b + c] = N;
+    if (!(p >= 0.f && p <= 1.f)) atomicAdd(bad_rows, 1);
+    term = -(y * fmaxf(logf(p), -100.f) + (1.f - y) * fmaxf(logf(1.f - p), -100.f));
+    gpred[c] = (p - y) / fmaxf((1.f - p) * p, 1e-12f) / float(b);
+  }
+  for (int o = 32; o > 0; o >>= 1) term += __shfl_xor(term, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = term;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    atomicAdd(loss_sum, t / float(b));
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Backward: same grid as the forward. Gradients are ADDED into the caller's buffers (fp32
 // atomics: the dense embedding grads by POI id, so repeated ids are summed as index_add does).
@@ -544,7 +582,9 @@ __global__ void train_reduce_kernel(const float* __restrict__ Wt, const float* _
                                     const float* __restrict__ Wh, int64_t b, int64_t n, int D,
                                     int H, int ns, int rb, const int64_t* __restrict__ hist,
                                     const int64_t* __restrict__ target, float* g_eh, float* g_et,
-                                    float* g_w1, float* g_b1, float* g_w2) {
+                                    float* g_w1, float* g_b1, float* g_w2,
+                                    const int32_t* __restrict__ bad_rows) {
+  if (bad_rows && *bad_rows) return;  // fused step on a NaN batch: no update (see train_loss)
   const int64_t wsz = int64_t(H) * D + 2 * H;
   const int64_t nblk = int64_t(ns) * rb;
   const int64_t nw = wsz * REDUCE_KS, nt = b * D, nh = n * D;
@@ -612,6 +652,176 @@ __global__ void adagrad_rows_kernel(float* __restrict__ p, float* __restrict__ s
     const float si = st[i] + gi * gi;
     st[i] = si;
     p[i] = p[i] + (-clr) * (gi / (sqrtf(si) + eps));
+  }
+}
+
+// Adagrad of the fused step, applied straight from the zero-maintained gradient scratch (which it
+// leaves zero again): the small tensors element-wise; the embedding tables row by row for the rows
+// the batch touched (history + targets; with weight_decay 0 the other rows' dense update is the
+// identity). A row listed twice is claimed once per step through `stamp` (atomicExch of the step
+// number), so it is updated once, with its summed gradient. One wave per row, lane = dim (D <= 64).
+struct StepOpt {
+  float* p_eh;
+  float* p_et;
+  float* p_small[3];  // w1, b1, w2
+  float* s_eh;
+  float* s_et;
+  float* s_small[3];
+  float* g_eh;
+  float* g_et;
+  float* g_small;  // [H*D | H | H]
+  int32_t* st_eh;
+  int32_t* st_et;
+  float clr, wd, eps;
+  int32_t tag;
+};
+
+__device__ __forceinline__ void adagrad_elem(float* p, float* st, float* g, float clr, float wd,
+                                             float eps) {
+  float gi = *g;
+  const float pi = *p;
+  if (wd != 0.f) gi = gi + wd * pi;
+  const float si = *st + gi * gi;
+  *st = si;
+  *p = pi + (-clr) * (gi / (sqrtf(si) + eps));
+  *g = 0.f;
+}
+
+__global__ void step_adagrad_kernel(StepOpt o, int H, int D, const int64_t* __restrict__ hist,
+                                    int64_t n, const int64_t* __restrict__ target, int64_t b,
+                                    int64_t dense_rows, const int32_t* __restrict__ bad_rows) {
+  if (*bad_rows) return;
+  const int64_t wsz = int64_t(H) * D + 2 * H;
+  const int64_t nsmall_blocks = (wsz + 255) / 256;
+  const int64_t bx = blockIdx.x;
+  if (bx < nsmall_blocks) {
+    const int64_t e = bx * 256 + threadIdx.x;
+    if (e < wsz) {
+      const int k = e < int64_t(H) * D ? 0 : (e < int64_t(H) * D + H ? 1 : 2);
+      const int64_t off = k == 0 ? e : (k == 1 ? e - int64_t(H) * D : e - int64_t(H) * D - H);
+      adagrad_elem(o.p_small[k] + off, o.s_small[k] + off, o.g_small + e, o.clr, o.wd, o.eps);
+    }
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t item = (bx - nsmall_blocks) * 4 + (threadIdx.x >> 6);
+  if (dense_rows > 0) {  // weight_decay != 0: every row of both tables changes
+    if (item >= 2 * dense_rows) return;
+    const bool tgt = item >= dense_rows;
+    const int64_t row = tgt ? item - dense_rows : item;
+    if (lane < D) {
+      const int64_t i = row * D + lane;
+      if (tgt) adagrad_elem(o.p_et + i, o.s_et + i, o.g_et + i, o.clr, o.wd, o.eps);
+      else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, o.wd, o.eps);
+    }
+    return;
+  }
+  if (item >= n + b) return;
+  const bool tgt = item >= n;
+  const int64_t row = tgt ? target[item - n] : hist[item];
+  int claimed = 0;
+  if (lane == 0) claimed = atomicExch(tgt ? o.st_et + row : o.st_eh + row, o.tag) != o.tag;
+  claimed = __shfl(claimed, 0);
+  if (claimed && lane < D) {
+    const int64_t i = row * D + lane;
+    if (tgt) adagrad_elem(o.p_et + i, o.s_et + i, o.g_et + i, o.clr, 0.f, o.eps);
+    else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, 0.f, o.eps);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Device-side get_NAIS_batch (batches.py:24-50) for one user: history = the
+// user's positives in a random order, rows [pos_i, neg_i1 .. neg_i,ng], labels 1 / 0. Negatives
+// are the first n*ng members, in a pseudo-random order of [0, P), that are not positives: a
+// uniformly random distinct subset of the complement, as the reference's shuffle-and-slice --
+// the same distribution, not Python's `random` stream. The orders come from a seeded Feistel
+// permutation of [0, 4^h) walked down to [0, m) (cycle walking), so no sort is needed.
+// ---------------------------------------------------------------------------------------------
+// 8-round Feistel network on [0, 2^(2*hb)) keyed by the seed (round function: murmur finaliser;
+// 8 rounds: 4 leave a visible bias on domains of a few elements)
+__device__ __forceinline__ uint32_t feistel(uint32_t x, int hb, uint32_t s) {
+  const uint32_t mh = (1u << hb) - 1u;
+  uint32_t L = x >> hb, R = x & mh;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t f = mix32(R ^ (s + uint32_t(r) * 0x9e3779b9u)) & mh;
+    const uint32_t t = L ^ f;
+    L = R;
+    R = t;
+  }
+  return (L << hb) | R;
+}
+
+// bijection of [0, m): the Feistel permutation of [0, 2^(2 hb)) >= m, walked until it lands < m
+__device__ __forceinline__ uint32_t permute(uint32_t i, uint32_t m, int hb, uint32_t s) {
+  do {
+    i = feistel(i, hb, s);
+  } while (i >= m);
+  return i;
+}
+
+// half the bits of the smallest power of two >= m (m >= 2), rounded up
+__device__ __forceinline__ int half_bits(uint32_t m) {
+  const int k = 32 - __clz(m - 1);
+  return (k + 1) >> 1;
+}
+
+constexpr int BATCH_THREADS = 1024;
+
+__global__ void __launch_bounds__(BATCH_THREADS)
+make_batch_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
+                  int64_t user, int64_t n, int64_t P, int ng, uint32_t s0, uint32_t s1,
+                  int64_t* __restrict__ hist, int64_t* __restrict__ target,
+                  float* __restrict__ labels, int32_t* __restrict__ err) {
+  __shared__ int32_t scan[BATCH_THREADS / 64];
+  __shared__ int64_t base;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t start = indptr[user];
+  if (tid == 0 && err && indptr[user + 1] - start != n) *err = 1;
+  const int64_t* row = indices + start;
+  const uint32_t mn = uint32_t(n), mP = uint32_t(P);
+  const int hn = mn > 1 ? half_bits(mn) : 0, hP = mP > 1 ? half_bits(mP) : 0;
+  for (int64_t i = tid; i < n; i += BATCH_THREADS) {
+    const int64_t v = row[mn > 1 ? permute(uint32_t(i), mn, hn, s0) : 0];
+    hist[i] = v;
+    target[i * (1 + ng)] = v;
+    labels[i * (1 + ng)] = 1.f;
+  }
+  if (tid == 0) base = 0;
+  __syncthreads();
+  const int64_t want = n * ng;
+  for (int64_t k0 = 0; k0 < n * (ng + 1); k0 += BATCH_THREADS) {
+    const int64_t k = k0 + tid;
+    int64_t cand = -1;
+    if (k < n * (ng + 1)) {
+      cand = mP > 1 ? permute(uint32_t(k), mP, hP, s1) : 0;
+      int64_t lo = 0, hi = n;  // binary search in the sorted CSR row
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (row[mid] < cand) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < n && row[lo] == cand) cand = -1;
+    }
+    const bool acc = cand >= 0;
+    const unsigned long long bal = __ballot(acc);
+    const int before = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) scan[w] = __popcll(bal);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int q = 0; q < BATCH_THREADS / 64; ++q) {
+      if (q < w) off += scan[q];
+      tot += scan[q];
+    }
+    const int64_t pos = base + off + before;
+    if (acc && pos < want) {
+      const int64_t r = pos / ng, q = pos % ng;
+      target[r * (1 + ng) + 1 + q] = cand;
+      labels[r * (1 + ng) + 1 + q] = 0.f;
+    }
+    __syncthreads();
+    if (tid == 0) base += tot;
+    __syncthreads();
   }
 }
 
@@ -727,6 +937,122 @@ int hip_rc(hipError_t e, const char* what) {
 
 extern "C" {
 
+size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
+  if (!params || b <= 0) return 0;
+  return nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);
+}
+
+int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
+                        const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
+                        int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
+                        int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+  TShape sh;
+  int rc = tvalidate(params, &sh);
+  if (rc) return rc;
+  if ((rc = check_batch(hist, n, target, b))) return rc;
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  if (!opt || !loss_sum || !bad_rows || (b > 0 && !labels))
+    return nais_internal_fail(NAIS_E_INVALID, "missing opt / loss_sum / bad_rows / labels");
+  if (!opt->sum_embed_history || !opt->sum_embed_target || !opt->sum_w1 || !opt->sum_b1 ||
+      !opt->sum_w2 || !opt->grad_embed_history || !opt->grad_embed_target || !opt->grad_small ||
+      !opt->stamp_embed_history || !opt->stamp_embed_target)
+    return nais_internal_fail(NAIS_E_INVALID, "nais_adagrad_state_t: missing buffer");
+  if (opt->step < 1) return nais_internal_fail(NAIS_E_INVALID, "opt->step must be >= 1");
+  if (b == 0) return NAIS_OK;
+  if (!workspace || workspace_bytes < nais_train_step_workspace_size(params, b, n))
+    return nais_internal_fail(NAIS_E_WORKSPACE, "workspace too small (nais_train_step_workspace_size)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* ws = static_cast<float*>(workspace);
+  float* saved = ws;            // [2b]
+  float* gpred = ws + 2 * b;    // [b]
+  float* own_pred = ws + 3 * b; // [b]
+  float* part = ws + 4 * b;     // forward partials, then backward partials
+  if (!pred) pred = own_pred;
+  const int D = params->embed_dim, H = params->hidden;
+  int64_t ns = 0, rb = (b + TROWS - 1) / TROWS;
+  int js = 1;
+  if (n > 0) {
+    js = slice_items(b, n, FWD_PER_CU);
+    ns = (n + js - 1) / js;
+    if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  }
+  const TrainArgs a = targs(params, hist, n, target, b, js, dropout_p, seed);
+  // 1. forward partials, 2. loss + dL/dpred
+  if (n > 0) {
+    NAIS_TRAIN_DISPATCH(launch_train_forward, sh, a, part, part + ns * b, st);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(train_loss_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
+                     part, part + ns * b, (int)ns, b, n, params->beta, labels, pred, saved, gpred,
+                     loss_sum, bad_rows);
+  if ((rc = nais_internal_check_launch("train_loss_kernel"))) return rc;
+  // 3. backward partials, 4. reduce into the zero-maintained gradient scratch
+  if (n > 0) {
+    float* Wt = part;
+    float* Ww = Wt + ns * b * D;
+    float* Wh = Ww + ns * rb * (int64_t(H) * D + 2 * H);
+    NAIS_TRAIN_DISPATCH(launch_train_backward, sh, a, saved, pred, gpred, Wt, Ww, Wh, st);
+    if (rc) return rc;
+    const int64_t total = (int64_t(H) * D + 2 * H) * REDUCE_KS + b * D + n * D;
+    float* gs = opt->grad_small;
+    hipLaunchKernelGGL(train_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       st, Wt, Ww, Wh, b, n, D, H, (int)ns, (int)rb, hist, target,
+                       opt->grad_embed_history, opt->grad_embed_target, gs, gs + int64_t(H) * D,
+                       gs + int64_t(H) * D + H, bad_rows);
+    if ((rc = nais_internal_check_launch("train_reduce_kernel"))) return rc;
+  }
+  // 5. Adagrad (run.py:89) straight from the scratch, which it zeroes again
+  StepOpt o;
+  o.p_eh = const_cast<float*>(params->embed_history);
+  o.p_et = const_cast<float*>(params->embed_target);
+  o.p_small[0] = const_cast<float*>(params->w1);
+  o.p_small[1] = const_cast<float*>(params->b1);
+  o.p_small[2] = const_cast<float*>(params->w2);
+  o.s_eh = opt->sum_embed_history;
+  o.s_et = opt->sum_embed_target;
+  o.s_small[0] = opt->sum_w1;
+  o.s_small[1] = opt->sum_b1;
+  o.s_small[2] = opt->sum_w2;
+  o.g_eh = opt->grad_embed_history;
+  o.g_et = opt->grad_embed_target;
+  o.g_small = opt->grad_small;
+  o.st_eh = opt->stamp_embed_history;
+  o.st_et = opt->stamp_embed_target;
+  o.clr = float(double(opt->lr) / (1.0 + double(opt->step - 1) * double(opt->lr_decay)));
+  o.wd = opt->weight_decay;
+  o.eps = opt->eps;
+  o.tag = int32_t(opt->step);
+  const int64_t wsz = int64_t(H) * D + 2 * H;
+  const int64_t dense = opt->weight_decay != 0.f ? params->num_pois : 0;
+  const int64_t rows = dense ? 2 * dense : n + b;
+  const int64_t blocks = (wsz + 255) / 256 + (rows + 3) / 4;
+  hipLaunchKernelGGL(step_adagrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, o, H, D, hist,
+                     n, target, b, dense, bad_rows);
+  return nais_internal_check_launch("step_adagrad_kernel");
+}
+
+int32_t nais_make_train_batch(const int64_t* indptr, const int64_t* indices, int64_t user,
+                              int64_t n, int64_t num_pois, int32_t num_ng, uint64_t seed,
+                              int64_t* hist, int64_t* target, float* labels, int32_t* err,
+                              void* stream) {
+  if (!indptr || !indices || user < 0 || n < 0 || num_ng < 0 || num_pois <= 0)
+    return nais_internal_fail(NAIS_E_INVALID, "bad arguments");
+  if (num_pois > 0x7fffffffll || n > 0x7fffffffll)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "num_pois / n must fit 31 bits");
+  if (n * (int64_t(num_ng) + 1) > num_pois)
+    return nais_internal_fail(NAIS_E_INVALID, "not enough negatives: n * (1 + num_ng) > num_pois");
+  if (n == 0) return NAIS_OK;
+  if (!hist || !target || !labels) return nais_internal_fail(NAIS_E_INVALID, "NULL output");
+  hipLaunchKernelGGL(make_batch_kernel, dim3(1), dim3(BATCH_THREADS), 0,
+                     reinterpret_cast<hipStream_t>(stream), indptr, indices, user, n, num_pois,
+                     (int)num_ng, mix32(uint32_t(seed) ^ 0x85ebca6bu),
+                     mix32(uint32_t(seed >> 32) ^ uint32_t(seed) * 0x9e3779b9u), hist, target,
+                     labels, err);
+  return nais_internal_check_launch("make_batch_kernel");
+}
+
 size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0 || n <= 0) return 0;
   const int js = slice_items(b, n, FWD_PER_CU);
@@ -802,7 +1128,7 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
   const int64_t total = (H * D + 2 * H) * REDUCE_KS + b * D + n * D;
   hipLaunchKernelGGL(train_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                      Wt, Ww, Wh, b, n, (int)D, (int)H, (int)ns, (int)rb, hist, target,
-                     grad_embed_history, grad_embed_target, grad_w1, grad_b1, grad_w2);
+                     grad_embed_history, grad_embed_target, grad_w1, grad_b1, grad_w2, nullptr);
   return nais_internal_check_launch("train_reduce_kernel");
 }
 

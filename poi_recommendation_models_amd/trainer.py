@@ -1,0 +1,160 @@
+"""The NAIS_basic training loop of run.py:91-111 on the device (SURVEY.md 8(f1) + 8(f2)).
+
+    for buid in shuffled users:                                   run.py:96-99
+        user_history, train_data, train_label = get_NAIS_batch(...)   batches.py:24-50  -> GPU
+        optimizer.zero_grad(); prediction = model(...)            run.py:102-103
+        loss = model.loss_func(...); loss.backward()              run.py:104-105     -> 1 call
+        train_loss += loss.item(); optimizer.step()               run.py:107-109
+
+`NAISTrainer.epoch(users)` runs that loop with two C-ABI calls per user -- `nais_make_train_batch`
+(device-side negative sampling) and `nais_train_step` (forward, BCELoss, backward, Adagrad) --
+and one host sync per epoch (the reference syncs on loss.item() every user). The model's
+parameters are updated in place; Adagrad's accumulators live in the trainer with torch's
+semantics (state 'sum' and 'step' per parameter, `optimizer_state()` exports them).
+
+The per-step arithmetic is the drop-in path's (NAIS_basic train-mode forward + backward +
+optim.Adagrad), differing only in fp32 summation order; tests/test_gpu_train.py checks both
+against the oracle. Batches follow get_NAIS_batch's distribution (shuffled positives as the
+shared history, num_ng distinct uniform negatives per positive), not Python's random stream.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _capi
+from .catalog import device_csr
+
+
+class NAISTrainer:
+    def __init__(self, model, train_matrix, lr=0.01, lr_decay=0.0, weight_decay=0.0, eps=1e-10,
+                 initial_accumulator_value=0.0, num_ng=4):
+        from .model import NAIS_basic
+        if not isinstance(model, NAIS_basic):
+            raise NotImplementedError("NAISTrainer: NAIS_basic only (SURVEY.md 8(f1))")
+        dev = model._check_device()
+        self.model, self.dev = model, dev
+        self.csr = device_csr(train_matrix, dev)
+        self.num_ng = int(num_ng)
+        self.lr, self.lr_decay, self.weight_decay, self.eps = lr, lr_decay, weight_decay, eps
+        self.step_count = 0
+        ps = dict(model.named_parameters())
+        self._names = ["embed_history.weight", "embed_target.weight", "attn_layer1.weight",
+                       "attn_layer1.bias", "attn_layer2.weight"]
+        self.sums = {k: torch.full_like(ps[k], initial_accumulator_value) for k in self._names}
+        P, D = ps["embed_history.weight"].shape
+        H = ps["attn_layer1.weight"].shape[0]
+        self._g_eh = torch.zeros(P, D, device=dev)
+        self._g_et = torch.zeros(P, D, device=dev)
+        self._g_small = torch.zeros(H * D + 2 * H, device=dev)
+        self._st_eh = torch.zeros(P, dtype=torch.int32, device=dev)
+        self._st_et = torch.zeros(P, dtype=torch.int32, device=dev)
+        self.loss_sum = torch.zeros(1, device=dev)
+        self.bad_rows = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._ws = torch.empty(0, dtype=torch.uint8, device=dev)
+        self._bufs = {}
+
+    # ------------------------------------------------------------------ batches (f2)
+    def batch(self, uid, seed=None):
+        """get_NAIS_batch(train_matrix, P, uid, num_ng) on the device: (hist [n], target [b],
+        labels [b]); the reference's user_history is hist repeated b times."""
+        n = int(self.csr.hist_len[uid])
+        b = n * (1 + self.num_ng)
+        key = (n, b)
+        if key not in self._bufs:
+            self._bufs = {key: (torch.empty(n, dtype=torch.int64, device=self.dev),
+                                torch.empty(b, dtype=torch.int64, device=self.dev),
+                                torch.empty(b, dtype=torch.float32, device=self.dev))}
+        hist, tgt, lab = self._bufs[key]
+        if seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+        lib = _capi.load()
+        _capi.check(lib.nais_make_train_batch(self.csr.indptr.data_ptr(), self.csr.indices.data_ptr(),
+                                              int(uid), n, self.csr.shape[1], self.num_ng, seed,
+                                              hist.data_ptr(), tgt.data_ptr(), lab.data_ptr(),
+                                              self._err.data_ptr(),
+                                              _capi.stream_handle(self.dev)), "nais_make_train_batch")
+        return hist, tgt, lab
+
+    # ------------------------------------------------------------------ one step (f1)
+    def _opt_struct(self):
+        o = _capi.NaisAdagradState()
+        o.lr, o.lr_decay, o.weight_decay, o.eps = self.lr, self.lr_decay, self.weight_decay, self.eps
+        o.step = self.step_count
+        s = self.sums
+        o.sum_embed_history = s["embed_history.weight"].data_ptr()
+        o.sum_embed_target = s["embed_target.weight"].data_ptr()
+        o.sum_w1 = s["attn_layer1.weight"].data_ptr()
+        o.sum_b1 = s["attn_layer1.bias"].data_ptr()
+        o.sum_w2 = s["attn_layer2.weight"].data_ptr()
+        o.grad_embed_history = self._g_eh.data_ptr()
+        o.grad_embed_target = self._g_et.data_ptr()
+        o.grad_small = self._g_small.data_ptr()
+        o.stamp_embed_history = self._st_eh.data_ptr()
+        o.stamp_embed_target = self._st_et.data_ptr()
+        return o
+
+    def step(self, hist, target, labels, dropout_seed=None, pred=None):
+        """One fused step on a get_NAIS_batch batch given as the shared history hist [n] (or the
+        reference's [b, n] user_history), target [b], labels [b]."""
+        m = self.model
+        if hist.dim() == 2:
+            hist = hist[0] if hist.shape[0] else hist.new_empty(0)
+        hist = hist.to(torch.int64).contiguous()
+        target = target.to(torch.int64).contiguous()
+        labels = labels.to(torch.float32).contiguous()
+        b, n = target.numel(), hist.numel()
+        p = float(m.drop.p) if m.training else 0.0
+        if dropout_seed is None:
+            dropout_seed = int(torch.randint(0, 2**62, (1,)).item())
+        self.step_count += 1
+        lib = _capi.load()
+        prm = m.nais_params()
+        need = lib.nais_train_step_workspace_size(prm, b, n)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(int(need * 1.25) + 256, dtype=torch.uint8, device=self.dev)
+        _capi.check(lib.nais_train_step(prm, self._opt_struct(), _capi.ptr(hist) if n else None, n,
+                                        _capi.ptr(target) if b else None, _capi.ptr(labels) if b else None,
+                                        b, p, dropout_seed, self.loss_sum.data_ptr(),
+                                        self.bad_rows.data_ptr(), _capi.ptr(pred),
+                                        self._ws.data_ptr(), self._ws.numel(),
+                                        _capi.stream_handle(self.dev)), "nais_train_step")
+
+    def epoch(self, users=None, shuffle=True):
+        """One pass of run.py:96-109 over `users` (default: every user, shuffled as run.py:96-97).
+        Returns train_loss (the sum of the per-user mean BCE losses, run.py:107)."""
+        if users is None:
+            users = np.arange(self.csr.shape[0])
+        users = np.asarray(users, dtype=np.int64)
+        if shuffle:
+            users = users[torch.randperm(len(users)).numpy()]
+        self.model.train()
+        self.loss_sum.zero_()
+        P = self.csr.shape[1]
+        for u in users.tolist():
+            n = int(self.csr.hist_len[u])
+            if n == 0:
+                continue   # empty batch: the reference's step changes nothing
+            if n * (1 + self.num_ng) > P:
+                raise ValueError(f"user {u}: {n} positives x {1 + self.num_ng} rows exceed {P} POIs "
+                                 "(get_NAIS_batch cannot draw enough negatives)")
+            self.step(*self.batch(u))
+        return self.finish()
+
+    def finish(self):
+        """Host sync: the accumulated loss; raises like the reference's BCELoss if a batch had a
+        NaN prediction (its update and all later ones were skipped)."""
+        bad = int(self.bad_rows.item())
+        if bad:
+            raise RuntimeError(f"all elements of input should be between 0 and 1 ({bad} NaN "
+                               "predictions: a single-item history equal to its target, "
+                               "model.py:92-95); the updates from that batch on were skipped")
+        if int(self._err.item()):
+            raise RuntimeError("nais_make_train_batch: history length disagrees with the CSR")
+        return float(self.loss_sum.item())
+
+    def optimizer_state(self):
+        """torch.optim.Adagrad-style per-parameter state {name: {'step', 'sum'}}."""
+        return {k: {"step": torch.tensor(float(self.step_count)), "sum": self.sums[k]}
+                for k in self._names}

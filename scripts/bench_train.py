@@ -4,6 +4,8 @@ BCELoss, backward, Adagrad (run.py:101-109) -- timed on one GPU.
 
 Legs (one JSON line):
   hip      NAIS_basic (train mode) + optim.Adagrad (row update), the reference's loop unchanged
+  fused    NAISTrainer.step: forward + BCELoss + backward + Adagrad in one C-ABI call
+  fused+batch  NAISTrainer.batch + step: get_NAIS_batch built on the device too (8(f2))
   kernels  the two training kernels alone (HIP events on the launch stream) with their MFMA
            FLOP rate: forward 2*H*D flops per pair, backward 3 x 2*H*D (u recompute, dx, dW1)
   torch    the reference's own op sequence (model.py:57-89 restated in eager PyTorch, autograd,
@@ -27,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 from poi_recommendation_models_amd import _capi, optim  # noqa: E402
 from poi_recommendation_models_amd.model import NAIS_basic  # noqa: E402
+from poi_recommendation_models_amd.trainer import NAISTrainer  # noqa: E402
 
 
 def batches(P, n, num_ng, count, seed):
@@ -122,6 +125,18 @@ def main():
     t = time_loop(hip_step, bs, a.warmup, a.steps)
     out["hip_ms_per_step"] = t * 1e3
 
+    # ---- fused native step (same batches), then with device-side batch construction
+    import scipy.sparse as sp
+    rows = np.repeat(np.arange(len(host)), a.n)
+    cols = np.concatenate([np.sort(h[0]) for h, _, _ in host])
+    X = sp.csr_matrix((np.ones(len(cols)), (rows, cols)), shape=(len(host), a.P))
+    tr = NAISTrainer(m, X, lr=0.01, num_ng=a.num_ng)
+    out["fused_ms_per_step"] = time_loop(lambda h, d, l: tr.step(h[0], d, l), bs, a.warmup, a.steps) * 1e3
+    users = [(u,) for u in range(len(host))]
+    out["fused_with_batch_ms_per_step"] = time_loop(lambda u: tr.step(*tr.batch(u)), users, a.warmup,
+                                                    a.steps) * 1e3
+    tr.finish()
+
     # ---- kernels alone, on their own stream, HIP events
     lib = _capi.load()
     prm = m.nais_params()
@@ -178,6 +193,7 @@ def main():
             topt.step()
         out["torch_eager_ms_per_step"] = time_loop(torch_step, bs, a.warmup, a.steps) * 1e3
         out["speedup_vs_torch_eager"] = out["torch_eager_ms_per_step"] / out["hip_ms_per_step"]
+        out["fused_speedup_vs_torch_eager"] = out["torch_eager_ms_per_step"] / out["fused_ms_per_step"]
 
     if a.cpu:
         sys.path.insert(0, ROOT)
