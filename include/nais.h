@@ -7,9 +7,11 @@
  *   nais_forward        replaces NAIS_basic.forward            model.py:40-55  (+ attention_network :57-89)
  *                                NAIS_regionEmbedding.forward   model.py:132-142 (+ :144-180)
  *                                NAIS_region_distance_Embedding.forward model.py:231-244 (+ :246-297)
+ *                                NAIS_distance_Embedding.forward model.py:340-353 (+ :355-395)
  *   nais_score_topk     replaces the per-user loop body of      validation.py:11-27 (NAIS_validation),
  *                                                               validation.py:38-55 (NAIS_region_validation),
- *                                                               validation.py:69-127 (NAIS_region_distance_validation)
+ *                                                               validation.py:69-127 (NAIS_region_distance_validation,
+ *                                                               also run with NAIS_distance_Embedding, run.py:431)
  *                       i.e. get_NAIS_batch_test* (batches.py:52-65, 110-139) + chunked forward + torch.topk
  *   nais_gather_rows    the embedding gather of model.py:64 (nn.Embedding -> index_select) as a standalone
  *                       HBM-roofline kernel
@@ -34,12 +36,13 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 4
+#define NAIS_ABI_VERSION 5
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
 #define NAIS_VARIANT_REGION 1          /* NAIS_regionEmbedding            model.py:99-187  */
 #define NAIS_VARIANT_REGION_DISTANCE 2 /* NAIS_region_distance_Embedding  model.py:189-304 */
+#define NAIS_VARIANT_DISTANCE 3        /* NAIS_distance_Embedding         model.py:306-408 */
 
 /* arithmetic of the W1 x products in the catalog scorer (nais_score_topk / nais_score_catalog) */
 #define NAIS_PRECISION_FP32 0          /* v_mfma_f32_32x32x2_f32: exact fp32 (k-ordered fmaf chain)           */
@@ -65,11 +68,11 @@ extern "C" {
  */
 typedef struct nais_params {
   int32_t variant;              /* NAIS_VARIANT_* */
-  int32_t embed_dim;            /* D: width of h_j (.) t. basic: embed_size; region*: embed_size      */
-  int32_t item_dim;             /* columns of embed_history/embed_target: D (basic) or D/2 (region*)  */
-  int32_t region_dim;           /* columns of embed_region: D/2 (region*), 0 (basic)                   */
+  int32_t embed_dim;            /* D: width of h_j (.) t (embed_size in every variant)                 */
+  int32_t item_dim;             /* columns of embed_history/embed_target: D (basic, distance), D/2 (region*) */
+  int32_t region_dim;           /* columns of embed_region: D/2 (region*), 0 (basic, distance)         */
   int32_t hidden;               /* H = attn_layer1.out_features (1..128)                               */
-  int32_t din;                  /* attn_layer1.in_features: D, or D+2 for region_distance              */
+  int32_t din;                  /* attn_layer1.in_features: D, or D+2 for region_distance / distance   */
   int64_t num_pois;             /* P = rows of embed_history / embed_target                            */
   int64_t num_regions;          /* R = rows of embed_region (0 for basic)                              */
   float beta;                   /* attention smoothing exponent (model.py:80), 0.5 in every driver     */
@@ -105,8 +108,9 @@ const char* nais_last_error(void);
  * or the logit of attention_network, exactly as model.py:57-89 (mask model.py:92-95, no
  * max-subtraction, beta-smoothed denominator). n == 0 gives logit 0.
  *   hist_region [b, n] (row stride hist_region_ld), target_region [b]: region variants only.
- *   target_lat_long [b, n, 2] f32 (row stride latlon_ld, in elements): region_distance only,
- *   = (|lat_c - lat_j|, |lng_c - lng_j|) as built at run.py:47-54 / validation.py:108-118.
+ *   target_lat_long [b, n, 2] f32 (row stride latlon_ld, in elements): region_distance and
+ *   distance, = (|lat_c - lat_j|, |lng_c - lng_j|) as built at run.py:47-54 / validation.py:108-118;
+ *   the kernels scale it x100 (model.py:265) or x1000 (distance, model.py:369) before dist_layer.
  *   nan_count (may be NULL): device int32, atomically incremented by the number of NaN logits
  *   (model.py:50-54 prints this count).
  */
@@ -126,7 +130,7 @@ int32_t nais_forward(const nais_params_t* params,
  * (score desc, POI id asc); NaN ranks first (torch.topk semantics).
  *   users[i] (i < num_users): user ids to score; out_ids / out_scores are [num_users, k].
  *   region_of [P] int64: POI -> region (businessRegionEmbedList, run.py:149-152), region variants.
- *   coords [P, 2] float64 (lat, lng): region_distance -- (|dlat|, |dlng|) formed on the fly in
+ *   coords [P, 2] float64 (lat, lng): (region_)distance -- (|dlat|, |dlng|) formed on the fly in
  *   float64, bit-identical to run.py:47-54. latlon_mat [P, P, 2] float64: the reference's own
  *   matrix (run.py:214), read instead when coords is NULL (feasible only for small P).
  *   k <= 1024 and every user needs at least k candidates (torch.topk raises otherwise; the

@@ -11,6 +11,7 @@ op for op, in the reference's order:
 * `forward_basic`              <- model.py:40-55 (NaN count + sigmoid)
 * `attention_region`           <- model.py:144-180 (NAIS_regionEmbedding.attention_network)
 * `attention_region_distance`  <- model.py:246-297 (NAIS_region_distance_Embedding.attention_network)
+* `attention_distance`         <- model.py:355-395 (NAIS_distance_Embedding.attention_network)
 * `complement_candidates`      <- batches.py:52-65 (set(range(P)) - set(history), ascending)
 * `catalog_scores_*`           <- validation.py:11-22 / 38-49 / 69-121 (chunked forward over all candidates)
 * `topk_ids`                   <- validation.py:26-27 (torch.topk + id lookup), with the build's
@@ -90,9 +91,10 @@ def attention_region(p, user_history, target_item, history_region, target_region
                            p["attn_layer2.weight"], beta)
 
 
-def dist_feature(p, target_lat_long):
-    """model.py:265: sigmoid(dist_layer(target_lat_long * 100)) -> [b,n,2] f32."""
-    ll = (np.asarray(target_lat_long, dtype=F32) * F32(100)).astype(F32)
+def dist_feature(p, target_lat_long, scale=100):
+    """model.py:265 (scale 100) / model.py:369 (scale 1000, NAIS_distance_Embedding):
+    sigmoid(dist_layer(target_lat_long * scale)) -> [b,n,2] f32."""
+    ll = (np.asarray(target_lat_long, dtype=F32) * F32(scale)).astype(F32)
     wd = p["dist_layer.weight"].astype(F32)
     bd = p["dist_layer.bias"].astype(F32)
     return _sigmoid(ll @ wd.T + bd)
@@ -107,6 +109,16 @@ def attention_region_distance(p, user_history, target_item, history_region, targ
     target = np.concatenate([p["embed_target.weight"][target_item],
                              er[target_region]], axis=-1)        # model.py:257-259
     dist = dist_feature(p, target_lat_long)                      # model.py:265
+    return _attention_tail(history, target, user_history, target_item,
+                           p["attn_layer1.weight"], p["attn_layer1.bias"],
+                           p["attn_layer2.weight"], beta, extra=dist)
+
+
+def attention_distance(p, user_history, target_item, target_lat_long, beta=0.5):
+    """model.py:355-395 (NAIS_distance_Embedding): basic embeddings + the x1000 distance feature."""
+    history = p["embed_history.weight"][user_history]            # model.py:361
+    target = p["embed_target.weight"][target_item]               # model.py:362
+    dist = dist_feature(p, target_lat_long, scale=1000)          # model.py:369
     return _attention_tail(history, target, user_history, target_item,
                            p["attn_layer1.weight"], p["attn_layer1.bias"],
                            p["attn_layer2.weight"], beta, extra=dist)
@@ -183,3 +195,17 @@ def topk_ids(cand, scores, k):
     order = np.lexsort((np.asarray(cand), -key, ~nanrank))
     order = order[:k]
     return np.asarray(cand)[order], np.asarray(scores)[order]
+
+
+def catalog_scores_distance(p, history, num_pois, coords, beta=0.5, chunk=2048):
+    """validation.py:69-121 run with NAIS_distance_Embedding (run.py:431): regions ignored."""
+    cand = complement_candidates(history, num_pois)
+    hist = np.asarray(history, dtype=np.int64)
+    out = np.empty(len(cand), dtype=F32)
+    for s in range(0, len(cand), chunk):
+        tg = cand[s:s + chunk]
+        uh = np.broadcast_to(hist, (len(tg), len(hist)))
+        tp = np.broadcast_to(tg.reshape(-1, 1), uh.shape)
+        ll = latlon_pairs(coords, tp, uh).astype(F32)
+        out[s:s + chunk] = _sigmoid(attention_distance(p, uh, tg, ll, beta))
+    return cand, out

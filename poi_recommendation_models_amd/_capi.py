@@ -12,9 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
-VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE = 0, 1, 2
+VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE, VARIANT_DISTANCE = 0, 1, 2, 3
 FLAG_SIGMOID = 1
 
 EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_topk_workspace_size",

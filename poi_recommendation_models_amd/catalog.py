@@ -77,11 +77,11 @@ def lpt_order(users, hist_len, num_pois):
 
 def _side_inputs(model, dev, region_of, coords, latlon_mat):
     reg = cor = llm = None
-    if model.VARIANT != _capi.VARIANT_BASIC:
+    if model.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE):
         if region_of is None:
             raise ValueError("region variants need businessRegionEmbedList (POI -> region)")
         reg = torch.as_tensor(np.asarray(region_of, dtype=np.int64)).to(dev)
-    if model.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+    if model.VARIANT in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE):
         if coords is not None:
             cor = torch.as_tensor(np.ascontiguousarray(coords, dtype=np.float64)).to(dev)
         elif latlon_mat is not None:

@@ -78,6 +78,15 @@ inline dim3 cat_grid(int64_t P, int nb, int cand_per_block) {
   return NAIS_TILE_MAJOR ? dim3((unsigned)nb, tiles) : dim3(tiles, (unsigned)nb);
 }
 
+// What each variant carries: the region half of the concatenation (model.py:153,157) and the
+// 2-feature distance input (model.py:265-267 at x100, model.py:369-371 at x1000).
+template <int VAR>
+struct VarT {
+  static constexpr bool REGION = VAR == NAIS_VARIANT_REGION || VAR == NAIS_VARIANT_REGION_DISTANCE;
+  static constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE || VAR == NAIS_VARIANT_DISTANCE;
+  static constexpr float DSCALE = VAR == NAIS_VARIANT_DISTANCE ? 1000.f : 100.f;
+};
+
 __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -195,12 +204,14 @@ __device__ __forceinline__ void item_step(const float4 (&t4)[DH / 4], HPtr hrow,
 // (|dlat|, |dlng|) is formed in float64 and cast to float32 as at run.py:51-52 / validation.py:118)
 struct DistW {
   float w0, w1, b;  // row hh of dist_layer: this lane half computes output feature hh
+  float scale;      // the variant's input scale (x100 / x1000)
 };
+template <int VAR>
 __device__ __forceinline__ DistW load_distw(const DevParams& p, int hh) {
-  return DistW{p.wd[2 * hh], p.wd[2 * hh + 1], p.bd[hh]};
+  return DistW{p.wd[2 * hh], p.wd[2 * hh + 1], p.bd[hh], VarT<VAR>::DSCALE};
 }
 __device__ __forceinline__ float dist_feature(const DistW& w, float ll0, float ll1) {
-  const float m0 = ll0 * 100.f, m1 = ll1 * 100.f;
+  const float m0 = ll0 * w.scale, m1 = ll1 * w.scale;
   return sigmoidf_ref(m0 * w.w0 + m1 * w.w1 + w.b);
 }
 
@@ -251,8 +262,8 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
                      const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                      const double* __restrict__ latlon_mat, float* __restrict__ scores,
                      int64_t score_ld, int32_t* __restrict__ nan_count) {
-  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool REGION = VarT<VAR>::REGION;
+  constexpr bool DIST = VarT<VAR>::DIST;
   constexpr int D = 2 * DH;
   using C = Consts<DH, HB, DIST>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -291,7 +302,7 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
     } else {
       llrow = latlon_mat + cc * p.P * 2;
     }
-    dw = load_distw(p, hh);
+    dw = load_distw<VAR>(p, hh);
   }
 
   float S = 0.f, N = 0.f;
@@ -368,8 +379,8 @@ forward_kernel(DevParams p, const int64_t* __restrict__ hist, int64_t b, int64_t
                int64_t hreg_ld, const int64_t* __restrict__ target_region,
                const float* __restrict__ latlon, int64_t ll_ld, float* __restrict__ out,
                int32_t* __restrict__ nan_count, int32_t flags) {
-  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool REGION = VarT<VAR>::REGION;
+  constexpr bool DIST = VarT<VAR>::DIST;
   using C = Consts<DH, HB, DIST>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float4* Aimg = reinterpret_cast<float4*>(smem);
@@ -392,7 +403,7 @@ forward_kernel(DevParams p, const int64_t* __restrict__ hist, int64_t b, int64_t
   }
   const int64_t* hrow_ids = hist + rr * hist_ld;
   DistW dw{0.f, 0.f, 0.f};
-  if (DIST) dw = load_distw(p, hh);
+  if (DIST) dw = load_distw<VAR>(p, hh);
   auto row_ptr = [&](int64_t j) -> const float* {
     const int64_t item = hrow_ids[j];
     if (REGION && hh) return p.er + hist_region[rr * hreg_ld + j] * p.region_dim;
@@ -571,8 +582,8 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
                         const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                         const double* __restrict__ latlon_mat, float* __restrict__ scores,
                         int64_t score_ld, int32_t* __restrict__ nan_count) {
-  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool REGION = VarT<VAR>::REGION;
+  constexpr bool DIST = VarT<VAR>::DIST;
   constexpr int D = 2 * DH;
   constexpr int KS = DH / 8;
   constexpr bool EREGS = HB <= 2 && DH <= 32;
@@ -654,7 +665,7 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
     } else {
       llrow = latlon_mat + cc * p.P * 2;
     }
-    dw = load_distw(p, hh);
+    dw = load_distw<VAR>(p, hh);
   }
 
   float S = 0.f, N = 0.f;
@@ -824,8 +835,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                          const double* __restrict__ latlon_mat, float* __restrict__ scores,
                          int64_t score_ld, int32_t* __restrict__ nan_count) {
-  constexpr bool REGION = VAR != NAIS_VARIANT_BASIC;
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool REGION = VarT<VAR>::REGION;
+  constexpr bool DIST = VarT<VAR>::DIST;
   using C = CfgB<DH, HB, DIST>;
   constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
   constexpr bool EREGS = HB <= 2 && DH <= 32;
@@ -915,7 +926,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     } else {
       llrow = latlon_mat + cc * p.P * 2;
     }
-    dw = load_distw(p, hh);
+    dw = load_distw<VAR>(p, hh);
   }
 
   float S = 0.f, N = 0.f;
@@ -1579,7 +1590,7 @@ struct Shape {
 
 int validate(const nais_params_t* p, Shape* sh) {
   if (!p) return fail(NAIS_E_INVALID, "params is NULL");
-  if (p->variant < 0 || p->variant > 2) return fail(NAIS_E_INVALID, "unknown variant");
+  if (p->variant < 0 || p->variant > 3) return fail(NAIS_E_INVALID, "unknown variant");
   if (p->precision != NAIS_PRECISION_FP32 && p->precision != NAIS_PRECISION_FP16X3 &&
       p->precision != NAIS_PRECISION_FP16X3_PAIRSPLIT)
     return fail(NAIS_E_INVALID, "unknown precision");
@@ -1593,6 +1604,10 @@ int validate(const nais_params_t* p, Shape* sh) {
   if (p->hidden <= 0 || p->hidden > 128) return fail(NAIS_E_UNSUPPORTED, "hidden must be in [1, 128]");
   if (p->variant == NAIS_VARIANT_BASIC) {
     if (p->item_dim != D || p->din != D) return fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
+  } else if (p->variant == NAIS_VARIANT_DISTANCE) {
+    if (p->item_dim != D || p->din != D + 2)
+      return fail(NAIS_E_INVALID, "distance: item_dim == embed_dim, din == embed_dim + 2");
+    if (!p->dist_w || !p->dist_b) return fail(NAIS_E_INVALID, "distance needs dist_layer weight and bias");
   } else {
     if (p->item_dim != D / 2 || p->region_dim != D / 2)
       return fail(NAIS_E_INVALID, "region variants: item_dim == region_dim == embed_dim/2");
@@ -1631,7 +1646,7 @@ int to_dev(const nais_params_t* p, DevParams* d) {
 
 template <int DH, int HB, int VAR>
 size_t catalog_lds() {
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool DIST = VarT<VAR>::DIST;
   return Consts<DH, HB, DIST>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
          (DIST ? size_t(JC) * 16 : 0);
 }
@@ -1657,7 +1672,7 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
 
 template <int DH, int HB, int VAR>
 size_t catalog_x3_lds() {
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool DIST = VarT<VAR>::DIST;
   return Consts16<DH, HB, DIST>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
          (DIST ? size_t(JC) * 16 : 0);
 }
@@ -1694,12 +1709,12 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream);
-  } else if constexpr (!(HB <= 2 && DH <= 32 && VAR != NAIS_VARIANT_REGION_DISTANCE)) {
+  } else if constexpr (!(HB <= 2 && DH <= 32 && !VarT<VAR>::DIST)) {
     // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel
     return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
                                           latlon_mat, scores, ld, nan_count, stream);
   } else {
-    const size_t lds = CfgB<DH, HB, VAR == NAIS_VARIANT_REGION_DISTANCE>::BYTES;
+    const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST>::BYTES;
     auto kern = catalog_score_x3b_kernel<DH, HB, VAR>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1719,7 +1734,7 @@ int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n
                    const int64_t* target, const int64_t* hreg, int64_t hreg_ld, const int64_t* treg,
                    const float* latlon, int64_t ll_ld, float* out, int32_t* nan_count, int32_t flags,
                    hipStream_t stream) {
-  constexpr bool DIST = VAR == NAIS_VARIANT_REGION_DISTANCE;
+  constexpr bool DIST = VarT<VAR>::DIST;
   const size_t lds = Consts<DH, HB, DIST>::BYTES;
   auto kern = forward_kernel<DH, HB, VAR>;
   static bool attr_set = false;
@@ -1740,7 +1755,8 @@ int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n
     switch (VAR_) {                                                               \
       case 0: NAIS_DISPATCH_DH(FN, DH_, HB_, 0, __VA_ARGS__); break;              \
       case 1: NAIS_DISPATCH_DH(FN, DH_, HB_, 1, __VA_ARGS__); break;              \
-      default: NAIS_DISPATCH_DH(FN, DH_, HB_, 2, __VA_ARGS__); break;             \
+      case 2: NAIS_DISPATCH_DH(FN, DH_, HB_, 2, __VA_ARGS__); break;              \
+      default: NAIS_DISPATCH_DH(FN, DH_, HB_, 3, __VA_ARGS__); break;             \
     }                                                                             \
   } while (0)
 #define NAIS_DISPATCH_DH(FN, DH_, HB_, V, ...)                                   \
@@ -1793,9 +1809,13 @@ int32_t nais_forward(const nais_params_t* params, const int64_t* hist, int64_t b
   if (b < 0 || n < 0) return fail(NAIS_E_INVALID, "negative b or n");
   if (b == 0) return NAIS_OK;
   if (!target || !out || (n > 0 && !hist)) return fail(NAIS_E_INVALID, "missing hist/target/out");
-  if (params->variant != NAIS_VARIANT_BASIC && (!target_region || (n > 0 && !hist_region)))
+  const bool region = params->variant == NAIS_VARIANT_REGION ||
+                      params->variant == NAIS_VARIANT_REGION_DISTANCE;
+  const bool dist = params->variant == NAIS_VARIANT_REGION_DISTANCE ||
+                    params->variant == NAIS_VARIANT_DISTANCE;
+  if (region && (!target_region || (n > 0 && !hist_region)))
     return fail(NAIS_E_INVALID, "region variants need hist_region and target_region");
-  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && n > 0 && !target_lat_long)
+  if (dist && n > 0 && !target_lat_long)
     return fail(NAIS_E_INVALID, "region_distance needs target_lat_long");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   DevParams d;
@@ -1833,9 +1853,11 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
   if (k <= 0 || k > MAX_K) return fail(NAIS_E_UNSUPPORTED, "k must be in [1, 1024]");
   if (!indptr || !indices || !users || !out_ids || !out_scores)
     return fail(NAIS_E_INVALID, "missing indptr/indices/users/outputs");
-  if (params->variant != NAIS_VARIANT_BASIC && !region_of)
+  if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
+      !region_of)
     return fail(NAIS_E_INVALID, "region variants need region_of");
-  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && !coords && !latlon_mat)
+  if ((params->variant == NAIS_VARIANT_REGION_DISTANCE || params->variant == NAIS_VARIANT_DISTANCE) &&
+      !coords && !latlon_mat)
     return fail(NAIS_E_INVALID, "region_distance needs coords or latlon_mat");
   if (prior && !prior->coords) return fail(NAIS_E_INVALID, "prior needs coords");
   const size_t need = nais_score_topk_workspace_size(params, num_users, k, prior != nullptr);
@@ -1893,9 +1915,11 @@ int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,
   if (num_users == 0) return NAIS_OK;
   if (!indptr || !indices || !users || !scores) return fail(NAIS_E_INVALID, "missing pointer");
   if (score_ld < params->num_pois) return fail(NAIS_E_INVALID, "score_ld < num_pois");
-  if (params->variant != NAIS_VARIANT_BASIC && !region_of)
+  if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
+      !region_of)
     return fail(NAIS_E_INVALID, "region variants need region_of");
-  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && !coords && !latlon_mat)
+  if ((params->variant == NAIS_VARIANT_REGION_DISTANCE || params->variant == NAIS_VARIANT_DISTANCE) &&
+      !coords && !latlon_mat)
     return fail(NAIS_E_INVALID, "region_distance needs coords or latlon_mat");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   DevParams d;

@@ -7,6 +7,8 @@ signatures follow the reference:
 * `NAIS_regionEmbedding(item_num, embed_size, hidden_size, beta, region_embed_size)`   model.py:99-187
 * `NAIS_region_distance_Embedding(item_num, embed_size, hidden_size, beta,
                                   region_embed_size, dist_embed_size)`                model.py:189-304
+* `NAIS_distance_Embedding(item_num, embed_size, hidden_size, beta,
+                           region_embed_size, dist_embed_size)`                       model.py:306-408
 
 `forward` evaluates attention_network + sigmoid on the device in one fused kernel
 (`nais_forward`); there is no CPU path: inputs must live on the ROCm device that holds the
@@ -115,14 +117,16 @@ class _NAISDevice(nn.Module):
         history, target = idx(history), idx(target).contiguous()
         b, n = history.shape
         ll, ll_ld = None, 0
-        if self.VARIANT != _capi.VARIANT_BASIC:
+        if self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE):
             if history_region is None or target_region is None:
                 raise ValueError("region variants need history_region and target_region")
             history_region = idx(history_region)
             target_region = idx(target_region).contiguous()
             if tuple(history_region.shape) != (b, n) or tuple(target_region.shape) != (b,):
                 raise ValueError("history_region must be [b, n] and target_region [b]")
-        if self.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+        else:
+            history_region = target_region = None
+        if self.VARIANT in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE):
             if target_lat_long is None or tuple(target_lat_long.shape) != (b, n, 2):
                 raise ValueError("target_lat_long must be [b, n, 2]")
             ll = target_lat_long.to(torch.float32)
@@ -360,3 +364,41 @@ class NAIS_region_distance_Embedding(_NAISDevice):
                           target_lat_long_tensor):
         return self._run_forward(user_history, target_item, history_region, target_region,
                                  target_lat_long_tensor, sigmoid=False)
+
+
+class NAIS_distance_Embedding(_NAISDevice):
+    """NAIS_basic + the distance feature sigmoid(dist_layer(1000 * (|dlat|, |dlng|))) appended to
+    h (.) t (model.py:306-408); the regions of forward() are accepted and ignored, as in the
+    reference. Validated by NAIS_region_distance_validation (run.py:431)."""
+    VARIANT = _capi.VARIANT_DISTANCE
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size, dist_embed_size):
+        super().__init__()
+        self.DEVICE = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_history = nn.Embedding(item_num, embed_size)
+        self.embed_target = nn.Embedding(item_num, embed_size)
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = BCELoss()
+        self.attn_layer1 = nn.Linear(embed_size + 2, hidden_size)
+        self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self.dist_layer = nn.Linear(2, 2)
+        self._init_weight_()
+
+    def _init_weight_(self):                                  # model.py:329-337
+        nn.init.normal_(self.embed_history.weight, std=0.01)
+        nn.init.normal_(self.embed_target.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def forward(self, history, target, history_region, target_region, target_distance):  # :339-353
+        return self._run_forward(history, target, target_lat_long=target_distance)
+
+    def attention_network(self, user_history, target_item, target_lat_long_tensor):     # :355-395
+        return self._run_forward(user_history, target_item, target_lat_long=target_lat_long_tensor,
+                                 sigmoid=False)

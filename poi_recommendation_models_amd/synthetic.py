@@ -106,13 +106,15 @@ def init_nais_params(num_pois: int, embed_size: int, hidden: int, seed: int = 0,
     p = {}
     if variant == "basic":
         d_item, din = embed_size, embed_size
+    elif variant == "distance":
+        d_item, din = embed_size, embed_size + 2
     else:
         d_item, din = embed_size // 2, embed_size
         if variant == "region_distance":
             din = embed_size + 2
     p["embed_history.weight"] = rng.normal(0, emb_std, (num_pois, d_item)).astype(f32)
     p["embed_target.weight"] = rng.normal(0, emb_std, (num_pois, d_item)).astype(f32)
-    if variant != "basic":
+    if variant not in ("basic", "distance"):
         p["embed_region.weight"] = rng.normal(0, emb_std, (num_regions, embed_size // 2)).astype(f32)
     b1 = 1.0 / np.sqrt(din)
     p["attn_layer1.weight"] = rng.uniform(-b1, b1, (hidden, din)).astype(f32)
@@ -120,8 +122,9 @@ def init_nais_params(num_pois: int, embed_size: int, hidden: int, seed: int = 0,
                              else np.zeros(hidden)).astype(f32)
     b2 = 1.0 / np.sqrt(hidden)
     p["attn_layer2.weight"] = rng.uniform(-b2, b2, (1, hidden)).astype(f32)
-    if variant == "region_distance":
-        p["embed_distance.weight"] = rng.normal(0, 0.01, (1, embed_size)).astype(f32)
+    if variant in ("region_distance", "distance"):
+        if variant == "region_distance":
+            p["embed_distance.weight"] = rng.normal(0, 0.01, (1, embed_size)).astype(f32)
         bd = 1.0 / np.sqrt(2.0)
         p["dist_layer.weight"] = rng.uniform(-bd, bd, (2, 2)).astype(f32)
         p["dist_layer.bias"] = (rng.normal(0, bias_std, 2) if bias_std > 0

@@ -17,7 +17,7 @@ def load_golden(name):
 
 def params_from(z, tag):
     pre = tag + "/"
-    return {k[len(pre):]: z[k] for k in z.files if k.startswith(pre) and k.count("/") == 1
+    return {k[len(pre):]: z[k] for k in z.files if k.startswith(pre) and "/" not in k[len(pre):]
             and ("." in k[len(pre):])}
 
 

@@ -30,6 +30,8 @@ def _model(variant, p, beta=0.5, precision="fp32"):
         m = M.NAIS_basic(P, din, H, beta)
     elif variant == "region":
         m = M.NAIS_regionEmbedding(P, din, H, beta, p["embed_region.weight"].shape[0])
+    elif variant == "distance":
+        m = M.NAIS_distance_Embedding(P, din - 2, H, beta, 10, 1)
     else:
         m = M.NAIS_region_distance_Embedding(P, din - 2, H, beta, p["embed_region.weight"].shape[0], 1)
     sd = m.state_dict()
@@ -78,6 +80,23 @@ def test_forward_region_golden(variant, tag, n):
     assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL
 
 
+@pytest.mark.parametrize("box", ["city", "tight"])
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 7])
+def test_forward_distance_golden(box, tag, n):
+    z = load_golden("forward_distance.npz")
+    m = _model("distance", params_from(z, f"{box}/{tag}"))
+    pre = f"{box}/{tag}/n{n}/"
+    hist, tgt, ref = z[pre + "hist"], z[pre + "target"], z[pre + "pred"]
+    c = z[f"{box}/coords"]
+    ll = np.abs(c[tgt][:, None, :] - c[hist])
+    zeros = _t(np.zeros_like(hist))
+    got = m(_t(hist), _t(tgt), zeros, zeros[:, 0], _t(ll, torch.float32)).cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL
+
+
 def test_forward_empty_history_and_expanded_rows():
     z = load_golden("forward_basic.npz")
     p = params_from(z, "trained")
@@ -99,11 +118,13 @@ def _catalog_kwargs(variant, z):
         return {}
     if variant == "region":
         return {"region_of": z["region_of"]}
+    if variant == "distance":
+        return {"coords": z["coords"]}
     return {"region_of": z["region_of"], "coords": z["coords"]}
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
-@pytest.mark.parametrize("variant", ["basic", "region", "region_distance"])
+@pytest.mark.parametrize("variant", ["basic", "region", "region_distance", "distance"])
 @pytest.mark.parametrize("tag", ["init", "trained"])
 def test_catalog_golden(variant, tag, precision):
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
@@ -166,6 +187,7 @@ def test_validation_dropin_metrics(precision):
     ("basic", 64, 128), ("basic", 128, 64), ("basic", 64, 20),
     ("region", 16, 32), ("region", 64, 64), ("region", 128, 128),
     ("region_distance", 16, 32), ("region_distance", 64, 64), ("region_distance", 128, 96),
+    ("distance", 16, 16), ("distance", 64, 64), ("distance", 128, 128),
 ])
 def test_catalog_vs_oracle_shapes(variant, D, H, precision):
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
@@ -176,9 +198,12 @@ def test_catalog_vs_oracle_shapes(variant, D, H, precision):
                          bias_std=0.1)
     m = _model(variant, p, precision=precision)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
-    kw = {} if variant == "basic" else {"region_of": data.region_of}
-    if variant == "region_distance":
-        kw["coords"] = data.place_coords
+    kw = {} if variant in ("basic", "distance") else {"region_of": data.region_of}
+    coords = data.place_coords
+    if variant == "distance":   # a 100x tighter box keeps the x1000 feature off saturation
+        coords = coords.mean(0) + (coords - coords.mean(0)) * 0.01
+    if variant in ("region_distance", "distance"):
+        kw["coords"] = coords
     full = score_catalog(m, csr, range(6), **kw).cpu().numpy()
     ids, sc = score_topk(m, csr, range(6), 50, **kw)
     ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
@@ -188,6 +213,8 @@ def test_catalog_vs_oracle_shapes(variant, D, H, precision):
             cand, ref = nais_oracle.catalog_scores_basic(p, h, P)
         elif variant == "region":
             cand, ref = nais_oracle.catalog_scores_region(p, h, P, data.region_of)
+        elif variant == "distance":
+            cand, ref = nais_oracle.catalog_scores_distance(p, h, P, coords)
         else:
             cand, ref = nais_oracle.catalog_scores_region_distance(p, h, P, data.region_of,
                                                                    data.place_coords)
@@ -196,6 +223,24 @@ def test_catalog_vs_oracle_shapes(variant, D, H, precision):
         rid, rsc = nais_oracle.topk_ids(cand, ref, 50)
         assert_topk_equivalent(rid, rsc, ids[u], sc[u], tie_eps=GPU_TIE_EPS,
                                lookup=dict(zip(cand.tolist(), ref.tolist())))
+
+
+def test_distance_validation_dropin():
+    """validation.NAIS_region_distance_validation with NAIS_distance_Embedding (run.py:431)."""
+    import scipy.sparse as sp
+    from poi_recommendation_models_amd import validation as V
+    z = load_golden("catalog_distance.npz")
+    m = _model("distance", params_from(z, "trained"))
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    X = sp.csr_matrix((np.ones(len(z["indices"])), z["indices"], z["indptr"]), shape=(U, P))
+
+    class Args:
+        topk = 50
+        powerlaw_weight = 0.2
+    got = V.NAIS_region_distance_validation(m, Args(), U, positives_from(z, "test"),
+                                            positives_from(z, "val"), X, z["region_of"], None,
+                                            [5, 10, 15, 20, 25, 30], poi_coords=z["coords"])
+    np.testing.assert_allclose(np.array(got), z["trained/metrics"], atol=2.0 / U)
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

@@ -51,6 +51,22 @@ def test_forward_region(variant, tag, n):
     np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
 
 
+@pytest.mark.parametrize("box", ["city", "tight"])
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 7])
+def test_forward_distance(box, tag, n):
+    """NAIS_distance_Embedding (model.py:306-408, x1000 distance scale)."""
+    z = load_golden("forward_distance.npz")
+    p = params_from(z, f"{box}/{tag}")
+    pre = f"{box}/{tag}/n{n}/"
+    hist, tgt, ref = z[pre + "hist"], z[pre + "target"], z[pre + "pred"]
+    ll = nais_oracle.latlon_pairs(z[f"{box}/coords"], np.broadcast_to(tgt[:, None], hist.shape), hist)
+    got = nais_oracle._sigmoid(nais_oracle.attention_distance(p, hist, tgt, ll.astype(np.float32)))
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+
+
 def _catalog(variant, z, p, u):
     P = int(z["num_pois"])
     hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
@@ -58,10 +74,12 @@ def _catalog(variant, z, p, u):
         return nais_oracle.catalog_scores_basic(p, hist, P)
     if variant == "region":
         return nais_oracle.catalog_scores_region(p, hist, P, z["region_of"])
+    if variant == "distance":
+        return nais_oracle.catalog_scores_distance(p, hist, P, z["coords"])
     return nais_oracle.catalog_scores_region_distance(p, hist, P, z["region_of"], z["coords"])
 
 
-@pytest.mark.parametrize("variant", ["basic", "region", "region_distance"])
+@pytest.mark.parametrize("variant", ["basic", "region", "region_distance", "distance"])
 @pytest.mark.parametrize("tag", ["init", "trained"])
 def test_catalog_topk(variant, tag):
     z = load_golden(f"catalog_{variant}.npz")
