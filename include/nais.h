@@ -194,6 +194,20 @@ int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, 
 int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
                          const int64_t* idx, int64_t m, float* out, void* stream);
 
+/*
+ * New4 family (model.py:1169-1306): the per-POI context tables its forward builds
+ * from the near-POI lists before NAIS_basic's attention (self_attention, model.py:1272-1295):
+ *   ext_history[p] = [embed_history[p] | result_in[p] | result_out[p]]   [P, embed_size]
+ *   ext_target[p]  = [embed_target[p]  | result_out[p] | result_in[p]]   [P, embed_size]
+ * embed_history / embed_target [P, embed_size/2], embed_ingoing / embed_outgoing [P, embed_size/4],
+ * near_pois [P, num_near] int64 (nearPOI, datasets.py:418). Scoring New4 is then the basic variant
+ * (nais_forward / nais_score_topk) with these two tables as embed_history / embed_target.
+ */
+int32_t nais_new4_tables(const float* embed_history, const float* embed_target,
+                         const float* embed_ingoing, const float* embed_outgoing,
+                         int64_t num_pois, int32_t embed_size, const int64_t* near_pois,
+                         int32_t num_near, float* ext_history, float* ext_target, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Training step of NAIS_basic on one get_NAIS_batch batch (batches.py:24-50):
  * b rows (target[b], int64 POI ids) that all share ONE history hist[n] (int64, the user's positives;

@@ -12,6 +12,8 @@ op for op, in the reference's order:
 * `attention_region`           <- model.py:144-180 (NAIS_regionEmbedding.attention_network)
 * `attention_region_distance`  <- model.py:246-297 (NAIS_region_distance_Embedding.attention_network)
 * `attention_distance`         <- model.py:355-395 (NAIS_distance_Embedding.attention_network)
+* `new4_tables`, `forward_new4` <- model.py:1212-1295 (New4: near-POI self_attention, then the
+                                  basic attention over the concatenated rows)
 * `complement_candidates`      <- batches.py:52-65 (set(range(P)) - set(history), ascending)
 * `catalog_scores_*`           <- validation.py:11-22 / 38-49 / 69-121 (chunked forward over all candidates)
 * `topk_ids`                   <- validation.py:26-27 (torch.topk + id lookup), with the build's
@@ -209,3 +211,44 @@ def catalog_scores_distance(p, history, num_pois, coords, beta=0.5, chunk=2048):
         ll = latlon_pairs(coords, tp, uh).astype(F32)
         out[s:s + chunk] = _sigmoid(attention_distance(p, uh, tg, ll, beta))
     return cand, out
+
+
+def _softmax(x):
+    x = np.asarray(x, dtype=F32)
+    e = np.exp(x - x.max(axis=-1, keepdims=True)).astype(F32)
+    return (e / e.sum(axis=-1, keepdims=True, dtype=F32)).astype(F32)
+
+
+def new4_tables(p, near, embed_size):
+    """model.py:1272-1295 + 1215-1222: ([P, D] history rows, [P, D] target rows)."""
+    near = np.asarray(near, dtype=np.int64)
+    ein = p["embed_ingoing.weight"].astype(F32)[near]           # [P, K, d4]
+    eout = p["embed_outgoing.weight"].astype(F32)[near]
+    P, K, d4 = ein.shape
+    scale = np.sqrt(F32(embed_size / 4)).astype(F32)             # torch.sqrt(torch.tensor(E/4))
+    q = ein[:, 0, :].reshape(P, 1, d4)
+    k_out = eout.reshape(P, d4, K)                               # reshape, not transpose
+    result_out = (_softmax(np.matmul(q, k_out) / scale) @ eout)[:, 0, :]
+    q = eout[:, 0, :].reshape(P, 1, d4)
+    k_in = ein.reshape(P, d4, K)
+    result_in = (_softmax(np.matmul(q, k_in) / scale) @ ein)[:, 0, :]
+    xh = np.concatenate([p["embed_history.weight"], result_in, result_out], -1).astype(F32)
+    xt = np.concatenate([p["embed_target.weight"], result_out, result_in], -1).astype(F32)
+    return xh, xt
+
+
+def _with_tables(p, xh, xt):
+    q = dict(p)
+    q["embed_history.weight"], q["embed_target.weight"] = xh, xt
+    return q
+
+
+def forward_new4(p, near, embed_size, user_history, target_item, beta=0.5):
+    xh, xt = new4_tables(p, near, embed_size)
+    return _sigmoid(attention_basic(_with_tables(p, xh, xt), user_history, target_item, beta))
+
+
+def catalog_scores_new4(p, near, embed_size, history, num_pois, beta=0.5):
+    """validation.py:254-272 (get_NAIS_batch_test_region candidates, chunked forward)."""
+    xh, xt = new4_tables(p, near, embed_size)
+    return catalog_scores_basic(_with_tables(p, xh, xt), history, num_pois, beta)

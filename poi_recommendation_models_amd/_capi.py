@@ -22,7 +22,7 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_distance_histogram", "nais_gather_rows", "nais_train_workspace_size",
            "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
            "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
-           "nais_make_train_batch")
+           "nais_make_train_batch", "nais_new4_tables")
 
 
 class NaisParams(ctypes.Structure):
@@ -120,6 +120,8 @@ def load(path: str | None = None):
                                     i64, vp, vp, i64, f32, u64, vp, vp, vp, vp, sz, vp]
     lib.nais_make_train_batch.restype = i32
     lib.nais_make_train_batch.argtypes = [vp, vp, i64, i64, i64, i32, u64, vp, vp, vp, vp, vp]
+    lib.nais_new4_tables.restype = i32
+    lib.nais_new4_tables.argtypes = [vp, vp, vp, vp, i64, i32, vp, i32, vp, vp, vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

@@ -9,6 +9,7 @@ signatures follow the reference:
                                   region_embed_size, dist_embed_size)`                model.py:189-304
 * `NAIS_distance_Embedding(item_num, embed_size, hidden_size, beta,
                            region_embed_size, dist_embed_size)`                       model.py:306-408
+* `New4(item_num, embed_size, hidden_size, beta, region_embed_size)`                  model.py:1169-1306
 
 `forward` evaluates attention_network + sigmoid on the device in one fused kernel
 (`nais_forward`); there is no CPU path: inputs must live on the ROCm device that holds the
@@ -24,6 +25,7 @@ the eval-only path for now (train-mode forward raises NotImplementedError).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -72,12 +74,17 @@ class _NAISDevice(nn.Module):
                 raise RuntimeError(f"{type(self).__name__}: parameter {n} must be contiguous float32")
         return dev
 
+    def _item_tables(self):
+        """(embed_history, embed_target) tables the kernels index by POI id."""
+        return self.embed_history.weight, self.embed_target.weight
+
     def nais_params(self) -> _capi.NaisParams:
         """`nais_params_t` view of this module's parameters (device pointers, no copies)."""
+        eh, et = self._item_tables()
         p = _capi.NaisParams()
         p.variant = self.VARIANT
         p.embed_dim = self.embed_size
-        p.item_dim = self.embed_history.weight.shape[1]
+        p.item_dim = eh.shape[1]
         p.region_dim = self.embed_region.weight.shape[1] if hasattr(self, "embed_region") else 0
         p.hidden = self.attn_layer1.weight.shape[0]
         p.din = self.attn_layer1.weight.shape[1]
@@ -86,8 +93,8 @@ class _NAISDevice(nn.Module):
         p.beta = float(self.beta)
         p.precision = {"fp32": _capi.PRECISION_FP32, "fp16x3": _capi.PRECISION_FP16X3,
                        "fp16x3_pairsplit": _capi.PRECISION_FP16X3_PAIRSPLIT}[self.precision]
-        p.embed_history = self.embed_history.weight.data_ptr()
-        p.embed_target = self.embed_target.weight.data_ptr()
+        p.embed_history = eh.data_ptr()
+        p.embed_target = et.data_ptr()
         p.embed_region = self.embed_region.weight.data_ptr() if hasattr(self, "embed_region") else None
         p.w1 = self.attn_layer1.weight.data_ptr()
         p.b1 = self.attn_layer1.bias.data_ptr()
@@ -402,3 +409,76 @@ class NAIS_distance_Embedding(_NAISDevice):
     def attention_network(self, user_history, target_item, target_lat_long_tensor):     # :355-395
         return self._run_forward(user_history, target_item, target_lat_long=target_lat_long_tensor,
                                  sigmoid=False)
+
+
+class New4(_NAISDevice):
+    """New4 (model.py:1169-1306): NAIS_basic's attention over POI rows extended with context
+    vectors from each POI's near-POI list. forward(history, target, near_pois, target_region)
+    builds the two [P, embed_size] tables on the device (`nais_new4_tables`, once per distinct
+    near_pois array and parameter version) and scores with the basic kernels. Eval only; the
+    unused sub-modules (embed_region, query/key/value, drop) are kept for state_dict parity."""
+    VARIANT = _capi.VARIANT_BASIC
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_ingoing = nn.Embedding(item_num, int(embed_size / 4))
+        self.embed_outgoing = nn.Embedding(item_num, int(embed_size / 4))
+        self.embed_history = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_target = nn.Embedding(item_num, int(embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = BCELoss()
+        self.softmax = nn.Softmax(dim=-1)
+        self.attn_layer1 = nn.Linear(embed_size, hidden_size)
+        self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self.query = nn.Linear(int(embed_size / 2), int(embed_size / 2))
+        self.key = nn.Linear(int(embed_size / 2), int(embed_size / 2))
+        self.value = nn.Linear(int(embed_size / 2), int(embed_size / 2))
+        self.drop = nn.Dropout()
+        self._init_weight_()
+        self._ext = None
+
+    def _init_weight_(self):                                  # model.py:1197-1209
+        for e in (self.embed_history, self.embed_target, self.embed_region, self.embed_ingoing,
+                  self.embed_outgoing):
+            nn.init.normal_(e.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def extended_tables(self, near_pois):
+        """([P, D] history rows, [P, D] target rows) for this near-POI array (cached)."""
+        dev = self._check_device()
+        near = torch.as_tensor(np.asarray(near_pois) if not torch.is_tensor(near_pois) else near_pois,
+                               dtype=torch.int64).to(dev).contiguous()
+        ws = (self.embed_history.weight, self.embed_target.weight, self.embed_ingoing.weight,
+              self.embed_outgoing.weight)
+        key = (near.data_ptr(), tuple(near.shape), tuple((w.data_ptr(), w._version) for w in ws))
+        if self._ext is not None and self._ext[0] == key:
+            return self._ext[1]
+        P, D = self.item_num, self.embed_size
+        if near.dim() != 2 or near.shape[0] != P:
+            raise ValueError(f"near_pois must be [{P}, K]")
+        xh = torch.empty(P, D, device=dev)
+        xt = torch.empty(P, D, device=dev)
+        _capi.check(_capi.load().nais_new4_tables(*[w.data_ptr() for w in ws], P, D, near.data_ptr(),
+                                                  near.shape[1], xh.data_ptr(), xt.data_ptr(),
+                                                  _capi.stream_handle(dev)), "nais_new4_tables")
+        self._ext = (key, (xh, xt), near)
+        return xh, xt
+
+    def _item_tables(self):
+        if self._ext is None:
+            raise RuntimeError("New4: call extended_tables(near_pois) (or forward) first")
+        return self._ext[1]
+
+    def forward(self, history, target, near_pois, target_region):   # model.py:1212-1222
+        if self.training:
+            raise NotImplementedError("New4: training mode is not implemented on the HIP path")
+        self.extended_tables(near_pois)
+        return self._run_forward(history, target)

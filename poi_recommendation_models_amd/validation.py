@@ -17,7 +17,7 @@ def recommend(model, args, num_users, train_matrix, **kw):
     model.eval()                                               # validation.py:8
     ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
     nan = int(model._last_nan.item())
-    if nan > 0:
+    if nan > 0 and type(model).__name__ == "NAIS_basic" and model.report_nan:
         print(nan)                                             # model.py:53-54
     return ids.cpu().tolist()
 
@@ -59,4 +59,17 @@ def NAIS_region_distance_validation(model, args, num_users, test_positive, val_p
     else:
         rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
                         latlon_mat=latlon_mat)
+    return _metrics(test_positive, val_positive, rec, k_list)
+
+
+def new4_validation(model, args, num_users, test_positive, val_positive, train_matrix,
+                    businessRegionEmbedList, k_list, nearPOI):
+    """validation.py:254-280 (New4): the context tables are built once (the reference rebuilds
+    them in every 1,024-candidate chunk), then every user's catalog is scored with the basic
+    kernels. Differs from the reference only where it breaks: with <= 1,024 candidates the
+    reference's chunk loop reads `pred` before assigning it (validation.py:264-266); here such
+    users are scored normally."""
+    model.eval()
+    model.extended_tables(nearPOI)
+    rec = recommend(model, args, num_users, train_matrix)
     return _metrics(test_positive, val_positive, rec, k_list)

@@ -20,7 +20,7 @@ def lib():
 def declared():
     src = open(os.path.join(ROOT, "include", "nais.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(nais_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(nais_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_exports_match_header(lib):

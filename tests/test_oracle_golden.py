@@ -153,3 +153,32 @@ def test_train_oracle_adagrad_matches_torch():
         opt.step()
         p, st = train_oracle.adagrad(p, st, g, 0.05, step, lr_decay=0.1, weight_decay=0.01)
     np.testing.assert_allclose(p, q.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 7])
+def test_forward_new4(tag, n):
+    """New4 (model.py:1169-1306) run by the reference with .cuda() as the identity."""
+    z = load_golden("new4_forward.npz")
+    p = params_from(z, tag)
+    hist, tgt, ref = z[f"{tag}/n{n}/hist"], z[f"{tag}/n{n}/target"], z[f"{tag}/n{n}/pred"]
+    got = nais_oracle.forward_new4(p, z["near"], p["attn_layer1.weight"].shape[1], hist, tgt)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+def test_catalog_new4(tag):
+    z = load_golden("new4_catalog.npz")
+    p = params_from(z, tag)
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    for u in range(U):
+        hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
+        cand, sc = nais_oracle.catalog_scores_new4(p, z["near"], 32, hist, P)
+        key = f"{tag}/full_scores_u{u}"
+        if key in z.files:
+            np.testing.assert_allclose(sc, z[key], rtol=0, atol=ORACLE_ATOL)
+        ids, top = nais_oracle.topk_ids(cand, sc, 50)
+        assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids, top,
+                               tie_eps=ORACLE_TIE_EPS, lookup=dict(zip(cand.tolist(), sc.tolist())))
