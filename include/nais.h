@@ -194,6 +194,37 @@ int32_t nais_topk_rows(const float* scores, int64_t score_ld, int64_t num_pois, 
 int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
                          const int64_t* idx, int64_t m, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * "Pairs" strategy of the full-catalog loop (validation.py:11-27). Every term of a user's score
+ * for history item j and candidate c depends on (j, c) only (model.py:57-89), so a user list's
+ * scores can be formed from two per-pair tables computed ONCE for the list's distinct history
+ * items instead of once per user:
+ *   nais_pair_rows     items[0 .. *num_items) = distinct history POIs of users[] (ascending),
+ *                      rowmap[P] = row of each POI in items[] or -1. Workspace:
+ *                      nais_pair_rows_workspace_size(P) bytes. *num_items is device memory.
+ *   nais_pair_table    for item rows r < num_items and candidates c in [col0, col0 + cols):
+ *                      e[r*ld + c-col0] = exp(a_rc) * [items[r] != c],  es[...] = e * (h_r . t_c),
+ *                      with the catalog kernels' arithmetic for params->precision (split-fp16
+ *                      where nais_score_catalog uses the fused split kernel, else exact fp32).
+ *   nais_pair_gather   for every user and c in [col0, col0 + cols): N = sum_j es[row(j), c],
+ *                      S = sum_j e[row(j), c] over the user's history in CSR order,
+ *                      scores[slot*score_ld + c] = sigmoid(N / S^beta) (history POIs = -1, empty
+ *                      history = 0.5); NaNs counted into *nan_count as nais_score_catalog does.
+ * The caller loops over column blocks sized to its memory budget and runs nais_topk_rows.
+ */
+size_t nais_pair_rows_workspace_size(int64_t num_pois);
+int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                       int32_t num_users, int64_t num_pois, int32_t* rowmap, int64_t* items,
+                       int64_t* num_items, void* workspace, size_t workspace_bytes, void* stream);
+int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                        int64_t col0, int64_t cols, const int64_t* region_of,
+                        const double* coords, const double* latlon_mat, float* e, float* es,
+                        int64_t ld, void* stream);
+int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
+                         const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                         int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
+                         int64_t score_ld, int32_t* nan_count, void* stream);
+
 /*
  * New4 family (model.py:1169-1306): the per-POI context tables its forward builds
  * from the near-POI lists before NAIS_basic's attention (self_attention, model.py:1272-1295):

@@ -22,7 +22,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_distance_histogram", "nais_gather_rows", "nais_train_workspace_size",
            "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
            "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
-           "nais_make_train_batch", "nais_new4_tables")
+           "nais_make_train_batch", "nais_new4_tables", "nais_pair_rows_workspace_size",
+           "nais_pair_rows", "nais_pair_table", "nais_pair_gather")
 
 
 class NaisParams(ctypes.Structure):
@@ -122,6 +123,15 @@ def load(path: str | None = None):
     lib.nais_make_train_batch.argtypes = [vp, vp, i64, i64, i64, i32, u64, vp, vp, vp, vp, vp]
     lib.nais_new4_tables.restype = i32
     lib.nais_new4_tables.argtypes = [vp, vp, vp, vp, i64, i32, vp, i32, vp, vp, vp]
+    lib.nais_pair_rows_workspace_size.restype = sz
+    lib.nais_pair_rows_workspace_size.argtypes = [i64]
+    lib.nais_pair_rows.restype = i32
+    lib.nais_pair_rows.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, sz, vp]
+    lib.nais_pair_table.restype = i32
+    lib.nais_pair_table.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp, vp,
+                                    i64, vp]
+    lib.nais_pair_gather.restype = i32
+    lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, vp, vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

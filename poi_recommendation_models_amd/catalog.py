@@ -91,8 +91,13 @@ def _side_inputs(model, dev, region_of, coords, latlon_mat):
     return reg, cor, llm
 
 
-def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlon_mat=None):
-    """Full score rows f32 [len(users), P] (history POIs = -1.0), via nais_score_catalog."""
+def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlon_mat=None,
+                  strategy="direct"):
+    """Full score rows f32 [len(users), P] (history POIs = -1.0), via nais_score_catalog
+    (strategy "direct") or the pair tables (strategy "pairs", nais_pair_*)."""
+    if strategy == "pairs":
+        return _score_topk_pairs(model, train_matrix, users, 1, region_of, coords, latlon_mat,
+                                 None, force=True, rows_only=True)
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model.embed_history.weight.shape[0]
@@ -110,15 +115,35 @@ def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlo
     return out
 
 
+# "pairs" strategy (include/nais.h): worth it when the listed users' history entries outnumber
+# their distinct history POIs by this factor (each (item, candidate) pair is then reused by that
+# many users on average); below it, the direct per-user kernels do less work.
+PAIR_MIN_SHARING = 3.0
+PAIR_MEMORY_FRACTION = 0.6      # of the device's free memory, for the tables + score rows
+
+
 def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlon_mat=None,
-               ordered=True, stream=None, prior=None):
+               ordered=True, stream=None, prior=None, strategy=None):
     """Top-k (ids int64 [len(users), k], scores f32) of every listed user over its complement
     candidates, ordered (score desc, POI id asc). Raises like torch.topk when a user has fewer
     than k candidates (validation.py:26).
 
     `prior` = (a, b, alpha, poi_coords): rank on the power-law-blended score
-    f32((1-alpha) * score) + alpha * G / max G instead (run.py:537-539, powerLaw.py:86-92)."""
+    f32((1-alpha) * score) + alpha * G / max G instead (run.py:537-539, powerLaw.py:86-92).
+
+    `strategy` (default: the model's `catalog_strategy`, "auto"): "direct" runs the fused per-user
+    kernels; "pairs" computes each (distinct history POI, candidate) term once and gathers every
+    user's sums from those tables (nais_pair_*); "auto" picks "pairs" when the users' history
+    entries outnumber their distinct POIs by PAIR_MIN_SHARING and there is no prior."""
     dev = model._check_device()
+    strategy = strategy or getattr(model, "catalog_strategy", "auto")
+    if strategy not in ("auto", "direct", "pairs"):
+        raise ValueError(f"unknown strategy {strategy!r}")
+    if strategy != "direct" and prior is None:
+        got = _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat,
+                                stream, force=strategy == "pairs")
+        if got is not None:
+            return got
     csr = device_csr(train_matrix, dev)
     P = model.embed_history.weight.shape[0]
     if csr.shape[1] != P:
@@ -160,6 +185,79 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
         inv_t = torch.from_numpy(inv).to(dev)
         ids, sc = ids.index_select(0, inv_t), sc.index_select(0, inv_t)
     return ids.to(torch.int64), sc
+
+
+def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
+                      rows_only=False):
+    dev = model._check_device()
+    csr = device_csr(train_matrix, dev)
+    P = model.embed_history.weight.shape[0]
+    if csr.shape[1] != P:
+        raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
+    users = np.asarray(list(users), dtype=np.int64)
+    n = len(users)
+    if n == 0:
+        return None
+    if np.any(P - csr.hist_len[users] < k):
+        raise RuntimeError("selected index k out of range")       # torch.topk's error
+    lib = _capi.load()
+    st = stream if stream is not None else _capi.stream_handle(dev)
+    u_all = torch.from_numpy(users.astype(np.int32)).to(dev)
+    reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
+    prm = model.nais_params()
+    rowmap = torch.empty(P, dtype=torch.int32, device=dev)
+    items = torch.empty(P, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = _workspace(dev, lib.nais_pair_rows_workspace_size(P))
+
+    def rows(u_dev, m):
+        _capi.check(lib.nais_pair_rows(csr.indptr.data_ptr(), csr.indices.data_ptr(), u_dev.data_ptr(),
+                                       m, P, rowmap.data_ptr(), items.data_ptr(), cnt.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), st), "nais_pair_rows")
+        return int(cnt.item())
+    J = rows(u_all, n)
+    entries = int(csr.hist_len[users].sum())
+    if not force and (J == 0 or entries < PAIR_MIN_SHARING * J):
+        return None
+    free = torch.cuda.mem_get_info(dev)[0]
+    budget = int(free * PAIR_MEMORY_FRACTION)
+    # users per pass: their score rows take at most half the budget
+    per_pass = n if rows_only else max(1, min(n, (budget // 2) // (4 * P)))
+    ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
+    sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
+    counters = torch.zeros(2, dtype=torch.int32, device=dev)
+    for b0 in range(0, n, per_pass):
+        m = min(per_pass, n - b0)
+        u_dev = u_all[b0:b0 + m]
+        if b0 > 0 or m < n:
+            J = rows(u_dev, m)
+        scores = torch.empty(m, P, dtype=torch.float32, device=dev)
+        if J > 0:
+            W = (budget // 2) // (8 * J)
+            W = int(min(P, max(256, W // 256 * 256)))
+            tab = torch.empty(2, J, W, dtype=torch.float32, device=dev)
+            for c0 in range(0, P, W):
+                cols = min(W, P - c0)
+                _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, cols, _capi.ptr(reg),
+                                                _capi.ptr(cor), _capi.ptr(llm), tab[0].data_ptr(),
+                                                tab[1].data_ptr(), W, st), "nais_pair_table")
+                _capi.check(lib.nais_pair_gather(tab[0].data_ptr(), tab[1].data_ptr(), W,
+                                                 rowmap.data_ptr(), csr.indptr.data_ptr(),
+                                                 csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, cols,
+                                                 float(model.beta), scores.data_ptr(), P,
+                                                 counters[0:1].data_ptr(), st), "nais_pair_gather")
+            del tab
+        else:
+            scores.fill_(0.5)   # every listed user has an empty history: logit 0 (model.py:79-88)
+        if rows_only:
+            model._last_nan = counters[0:1]
+            return scores
+        _capi.check(lib.nais_topk_rows(scores.data_ptr(), P, P, m, k, ids_out[b0:b0 + m].data_ptr(),
+                                       sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(), st),
+                    "nais_topk_rows")
+        del scores
+    model._last_nan = counters[0:1]
+    return ids_out.to(torch.int64), sc_out
 
 
 def prior_rows(train_matrix, users, a, b, coords, device):

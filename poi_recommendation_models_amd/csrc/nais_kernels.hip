@@ -47,6 +47,7 @@ constexpr int JC = 64;                      // history rows staged in LDS per ch
 constexpr int TOPK_THREADS = 1024;
 constexpr int MAX_K = 1024;
 constexpr int MAX_BATCH_USERS = 512;        // users scored per catalog launch
+constexpr int PAIR_GROUP_ITEMS = 128;       // item rows per workgroup in pair-table mode
 
 struct DevParams {
   const float* eh;
@@ -62,6 +63,19 @@ struct DevParams {
   float beta;
 };
 
+// Pair-table mode of the catalog kernels ("pairs" strategy): instead of summing over
+// one user's history, a workgroup takes `gi` consecutive rows of an item list (indices[0..nitems))
+// and writes, for every (item row r, candidate c) with c in [col0, col0 + cols),
+//   e = exp(a) * [item != c]  to e[r * ld + c - col0]   and   e * (h . t)  to es[...]
+// -- all a user needs from the pair: pair_gather_kernel sums them over each user's history rows.
+// e == nullptr: the normal per-user scoring.
+struct TableOut {
+  float* e = nullptr;
+  float* es = nullptr;
+  int64_t ld = 0, col0 = 0, cols = 0, nitems = 0;
+  int32_t gi = 0;
+};
+
 #ifndef NAIS_TILE_MAJOR
 #define NAIS_TILE_MAJOR 0
 #endif
@@ -73,6 +87,9 @@ struct DevParams {
 // Infinity Cache serves the re-reads at ~40 GB/s, far below any limit.
 __device__ __forceinline__ int cat_user_slot() { return NAIS_TILE_MAJOR ? blockIdx.x : blockIdx.y; }
 __device__ __forceinline__ int cat_tile() { return NAIS_TILE_MAJOR ? blockIdx.y : blockIdx.x; }
+inline dim3 table_grid(const TableOut& t, int ngroups) {
+  return dim3((unsigned)((t.cols + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)ngroups);
+}
 inline dim3 cat_grid(int64_t P, int nb, int cand_per_block) {
   const unsigned tiles = (unsigned)((P + cand_per_block - 1) / cand_per_block);
   return NAIS_TILE_MAJOR ? dim3((unsigned)nb, tiles) : dim3(tiles, (unsigned)nb);
@@ -261,7 +278,7 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
                      const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                      const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                      const double* __restrict__ latlon_mat, float* __restrict__ scores,
-                     int64_t score_ld, int32_t* __restrict__ nan_count) {
+                     int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
   constexpr bool REGION = VarT<VAR>::REGION;
   constexpr bool DIST = VarT<VAR>::DIST;
   constexpr int D = 2 * DH;
@@ -275,11 +292,17 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JC);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[cat_user_slot()];
-  const int64_t hbeg = indptr[u];
-  const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
-  const bool valid = c < p.P;
+  int64_t hbeg, hlen;
+  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
+    hbeg = (int64_t)cat_user_slot() * tab.gi;
+    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  } else {
+    const int64_t u = users[cat_user_slot()];
+    hbeg = indptr[u];
+    hlen = indptr[u + 1] - hbeg;
+  }
+  const int64_t c = tab.col0 + (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P && (!tab.e || c < tab.col0 + tab.cols);
   const int64_t cc = valid ? c : p.P - 1;
 
   stage_consts<DH, HB, DIST>(p, Aimg, Adist, Eimg, tid);
@@ -350,11 +373,20 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
       item_step<DH, HB, DIST>(t4, hrows + jj * D + hh * DH, Aimg, Adist, epi, distf, lane, a, s);
       const bool keep = hid[jj] != (int32_t)c;             // model.py:92-95
       const float e = expf(a) * (keep ? 1.f : 0.f);        // model.py:75-78 (inf * 0 -> NaN)
+      if (tab.e) {
+        if (valid && hh == 0) {
+          const int64_t o = (hbeg + j0 + jj) * tab.ld + (c - tab.col0);
+          tab.e[o] = e;
+          tab.es[o] = e * s;
+        }
+        continue;
+      }
       in_hist |= !keep;
       S += e;                                               // model.py:79
       N += e * s;                                           // sum_j w_j (h_j . t) numerator
     }
   }
+  if (tab.e) return;
 
   const float logit = finish_logit(S, N, p.beta, hlen == 0);
   const bool isnan_ = logit != logit;
@@ -581,7 +613,7 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
                         const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                         const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                         const double* __restrict__ latlon_mat, float* __restrict__ scores,
-                        int64_t score_ld, int32_t* __restrict__ nan_count) {
+                        int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
   constexpr bool REGION = VarT<VAR>::REGION;
   constexpr bool DIST = VarT<VAR>::DIST;
   constexpr int D = 2 * DH;
@@ -598,11 +630,17 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JC);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[cat_user_slot()];
-  const int64_t hbeg = indptr[u];
-  const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
-  const bool valid = c < p.P;
+  int64_t hbeg, hlen;
+  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
+    hbeg = (int64_t)cat_user_slot() * tab.gi;
+    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  } else {
+    const int64_t u = users[cat_user_slot()];
+    hbeg = indptr[u];
+    hlen = indptr[u + 1] - hbeg;
+  }
+  const int64_t c = tab.col0 + (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P && (!tab.e || c < tab.col0 + tab.cols);
   const int64_t cc = valid ? c : p.P - 1;
 
   // ---- W1 scale, then the split A image (hi/lo per 8-dim slice) and the fp32 distance columns
@@ -834,7 +872,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                          const int64_t* __restrict__ region_of, const double* __restrict__ coords,
                          const double* __restrict__ latlon_mat, float* __restrict__ scores,
-                         int64_t score_ld, int32_t* __restrict__ nan_count) {
+                         int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
   constexpr bool REGION = VarT<VAR>::REGION;
   constexpr bool DIST = VarT<VAR>::DIST;
   using C = CfgB<DH, HB, DIST>;
@@ -850,11 +888,17 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   double* hco = reinterpret_cast<double*>(hid + JCB);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t u = users[cat_user_slot()];
-  const int64_t hbeg = indptr[u];
-  const int64_t hlen = indptr[u + 1] - hbeg;
-  const int64_t c = (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
-  const bool valid = c < p.P;
+  int64_t hbeg, hlen;
+  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
+    hbeg = (int64_t)cat_user_slot() * tab.gi;
+    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  } else {
+    const int64_t u = users[cat_user_slot()];
+    hbeg = indptr[u];
+    hlen = indptr[u + 1] - hbeg;
+  }
+  const int64_t c = tab.col0 + (int64_t)cat_tile() * CAND_PER_BLOCK + wave * 32 + (lane & 31);
+  const bool valid = c < p.P && (!tab.e || c < tab.col0 + tab.cols);
   const int64_t cc = valid ? c : p.P - 1;
 
   // ---- this thread's W1 values for the fragment entries it builds (fp32, unscaled)
@@ -964,6 +1008,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   };
 
   float Sacc = 1.f, invS = 1.f;
+  int64_t j0 = 0;   // history chunk base (the step's table-mode write needs it)
 
   // One pipeline step: the MFMA chain of item `cur` (A_j from the ring slot `src`, t_c from VGPRs)
   // into accN, with the VALU epilogue of the previous item (accP, chunk-local `prev`) cut into KS
@@ -1030,15 +1075,23 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const bool keep = hid[pj] != (int32_t)c;
     const float e = expf(a) * (keep ? 1.f : 0.f);
     if (live) {
-      in_hist |= !keep;
-      S += e;
-      N += e * sv;
+      if (tab.e) {
+        if (valid && hh == 0) {
+          const int64_t o = (hbeg + j0 + pj) * tab.ld + (c - tab.col0);
+          tab.e[o] = e;
+          tab.es[o] = e * sv;
+        }
+      } else {
+        in_hist |= !keep;
+        S += e;
+        N += e * sv;
+      }
     }
   };
 
   float SAcur = 1.f;
   floatx16 accP[HB];
-  for (int64_t j0 = 0; j0 < hlen; j0 += JCB) {
+  for (j0 = 0; j0 < hlen; j0 += JCB) {
     const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
     __syncthreads();
     float hmax = 0.f;
@@ -1104,6 +1157,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       step(std::false_type{}, ring, accN, accP, 0, prev, true);
     }
   }
+  if (tab.e) return;
 
   const float logit = finish_logit(S, N, p.beta, hlen == 0);
   const bool isnan_ = logit != logit;
@@ -1655,7 +1709,7 @@ template <int DH, int HB, int VAR>
 int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                    const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                    const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
-                   hipStream_t stream) {
+                   hipStream_t stream, const TableOut& tab = TableOut{}) {
   const size_t lds = catalog_lds<DH, HB, VAR>();
   auto kern = catalog_score_kernel<DH, HB, VAR>;
   static bool attr_set = false;
@@ -1664,9 +1718,9 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
+  dim3 grid = tab.e ? table_grid(tab, nb) : cat_grid(d.P, nb, CAND_PER_BLOCK);
   hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
-                     coords, latlon_mat, scores, ld, nan_count);
+                     coords, latlon_mat, scores, ld, nan_count, tab);
   return check_launch("catalog_score_kernel");
 }
 
@@ -1696,7 +1750,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
     }
     dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
-                       coords, latlon_mat, scores, ld, nan_count);
+                       coords, latlon_mat, scores, ld, nan_count, TableOut{});
     return check_launch("catalog_score_x3_kernel");
   }
 }
@@ -1705,11 +1759,14 @@ template <int DH, int HB, int VAR>
 int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                        const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                        const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
-                       hipStream_t stream) {
+                       hipStream_t stream, const TableOut& tab = TableOut{}) {
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
-                                       scores, ld, nan_count, stream);
+                                       scores, ld, nan_count, stream, tab);
   } else if constexpr (!(HB <= 2 && DH <= 32 && !VarT<VAR>::DIST)) {
+    if (tab.e)   // table mode has no per-pair split variant: exact fp32 kernel
+      return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
+                                         latlon_mat, scores, ld, nan_count, stream, tab);
     // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel
     return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
                                           latlon_mat, scores, ld, nan_count, stream);
@@ -1722,9 +1779,9 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
+    dim3 grid = tab.e ? table_grid(tab, nb) : cat_grid(d.P, nb, CAND_PER_BLOCK);
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
-                       coords, latlon_mat, scores, ld, nan_count);
+                       coords, latlon_mat, scores, ld, nan_count, tab);
     return check_launch("catalog_score_x3b_kernel");
   }
 }
@@ -1899,6 +1956,51 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
       rc = check_launch("topk_blend_kernel");
       if (rc) return rc;
     }
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                        int64_t col0, int64_t cols, const int64_t* region_of,
+                        const double* coords, const double* latlon_mat, float* e, float* es,
+                        int64_t ld, void* stream) {
+  Shape sh;
+  int rc = validate(params, &sh);
+  if (rc) return rc;
+  if (num_items < 0 || col0 < 0 || cols < 0 || col0 + cols > params->num_pois)
+    return fail(NAIS_E_INVALID, "bad item count or column range");
+  if (num_items == 0 || cols == 0) return NAIS_OK;
+  if (!items || !e || !es) return fail(NAIS_E_INVALID, "missing pointer");
+  if (ld < cols) return fail(NAIS_E_INVALID, "ld < cols");
+  if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
+      !region_of)
+    return fail(NAIS_E_INVALID, "region variants need region_of");
+  if ((params->variant == NAIS_VARIANT_REGION_DISTANCE || params->variant == NAIS_VARIANT_DISTANCE) &&
+      !coords && !latlon_mat)
+    return fail(NAIS_E_INVALID, "distance variants need coords or latlon_mat");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DevParams d;
+  rc = to_dev(params, &d);
+  if (rc) return rc;
+  TableOut tab;
+  tab.ld = ld;
+  tab.cols = cols;
+  tab.gi = PAIR_GROUP_ITEMS;
+  const int64_t groups_per_launch = 65535;
+  for (int64_t g0 = 0; g0 * tab.gi < num_items; g0 += groups_per_launch) {
+    const int64_t base = g0 * tab.gi;
+    tab.nitems = std::min<int64_t>(num_items - base, groups_per_launch * tab.gi);
+    tab.e = e + base * ld;
+    tab.es = es + base * ld;
+    tab.col0 = col0;
+    const int ng = (int)((tab.nitems + tab.gi - 1) / tab.gi);
+    if (params->precision == NAIS_PRECISION_FP32)
+      NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, nullptr, items + base, nullptr,
+                    ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
+    else
+      NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, nullptr, items + base,
+                    nullptr, ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
+    if (rc) return rc;
   }
   return NAIS_OK;
 }

@@ -1,0 +1,252 @@
+// nais_pairs.hip -- the "pairs" strategy of full-catalog scoring.
+//
+// Every term of a user's score, for history item j and candidate c (validation.py:11-27 over
+// model.py:57-89), depends on (j, c) only:
+//   e_jc = exp(w2 . ReLU(W1 (h_j (.) t_c) + b1)) [j != c],   s_jc = h_j . t_c
+//   logit_uc = sum_{j in H_u} e_jc s_jc / (sum_{j in H_u} e_jc)^beta
+// At the bench geometry each (j, c) pair is shared by sum_u h_u / P ~ 50 users, so the catalog
+// kernels in pair-table mode (nais_pair_table) evaluate the MLP once per pair of the users'
+// distinct history items x a column block of candidates, and this file's pair_gather_kernel
+// forms each user's N = sum e s and S = sum e by streaming the user's h_u table rows from HBM
+// (coalesced 16-byte loads; the history-gather kernel of the north star). Same per-pair
+// arithmetic, same j order of the sums as the direct kernels.
+//
+//   nais_pair_rows    distinct history items of a user list -> items[] + rowmap[P] (POI -> row)
+//   nais_pair_gather  per user: scores[c] for c in a column block from the tables
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "nais.h"
+#include "nais_internal.h"
+
+namespace {
+
+typedef float nf4 __attribute__((ext_vector_type(4)));
+
+#ifndef NAIS_GATHER_NT
+#define NAIS_GATHER_NT 0   // 1: non-temporal table loads (slower: the Infinity Cache then holds nothing)
+#endif
+__device__ __forceinline__ nf4 load4(const float* p) {
+  if (NAIS_GATHER_NT) return __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+  return *reinterpret_cast<const nf4*>(p);
+}
+
+constexpr int SCAN_THREADS = 1024;
+
+__global__ void mark_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
+                            const int32_t* __restrict__ users, int32_t* __restrict__ flag) {
+  const int64_t u = users[blockIdx.x];
+  for (int64_t i = indptr[u] + threadIdx.x; i < indptr[u + 1]; i += blockDim.x) flag[indices[i]] = 1;
+}
+
+__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int q = 0; q < SCAN_THREADS / 64; ++q) {
+      const int t = sh[q];
+      sh[q] = run;
+      run += t;
+    }
+    sh[SCAN_THREADS / 64] = run;
+  }
+  __syncthreads();
+  total = sh[SCAN_THREADS / 64];
+  const int r = x - v + sh[w];
+  __syncthreads();
+  return r;
+}
+
+// per-block counts of flagged POIs
+__global__ void __launch_bounds__(SCAN_THREADS)
+count_kernel(const int32_t* __restrict__ flag, int64_t P, int32_t* __restrict__ bsum) {
+  __shared__ int sh[SCAN_THREADS / 64 + 1];
+  const int64_t p = int64_t(blockIdx.x) * SCAN_THREADS + threadIdx.x;
+  int total;
+  block_excl_scan(p < P ? flag[p] : 0, sh, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// exclusive scan of the block counts (one workgroup, any number of blocks)
+__global__ void __launch_bounds__(SCAN_THREADS)
+scan_blocks_kernel(int32_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ count) {
+  __shared__ int sh[SCAN_THREADS / 64 + 1];
+  int64_t run = 0;
+  for (int64_t b0 = 0; b0 < nb; b0 += SCAN_THREADS) {
+    const int64_t b = b0 + threadIdx.x;
+    const int v = b < nb ? bsum[b] : 0;
+    int total;
+    const int ex = block_excl_scan(v, sh, total);
+    if (b < nb) bsum[b] = int32_t(run + ex);
+    run += total;
+  }
+  if (threadIdx.x == 0) *count = run;
+}
+
+// rowmap[p] = row of POI p in items[] (ascending POI order), -1 if p is in no history
+__global__ void __launch_bounds__(SCAN_THREADS)
+place_kernel(int32_t* __restrict__ flag_rowmap, int64_t P, const int32_t* __restrict__ bsum,
+             int64_t* __restrict__ items) {
+  __shared__ int sh[SCAN_THREADS / 64 + 1];
+  const int64_t p = int64_t(blockIdx.x) * SCAN_THREADS + threadIdx.x;
+  const int f = p < P ? flag_rowmap[p] : 0;
+  int total;
+  const int ex = block_excl_scan(f, sh, total);
+  if (p < P) {
+    const int row = bsum[blockIdx.x] + ex;
+    flag_rowmap[p] = f ? row : -1;
+    if (f) items[row] = p;
+  }
+}
+
+// One wave per user, 4 users per workgroup; a wave covers a 256-column stripe (4 columns per
+// lane). Grid x = user groups (fastest), y = stripes: the workgroups in flight read the same
+// stripe of the tables -- J x 256 x 8 B, ~200 MB at J = 100k -- so the Infinity Cache serves the
+// rows the ~50 users sharing each item read (A/B: profiles/r1/pairs/). N and S are summed in
+// history (CSR) order, then the score of model.py:55 / validation.py:26; history POIs get -1.
+constexpr int GW = 4;                       // users (waves) per workgroup
+
+// lane jj's 64-bit value, as a wave-uniform scalar (readlane returns int: widen via uint32_t)
+__device__ __forceinline__ int64_t bcast64(uint32_t lo, uint32_t hi, int jj) {
+  const uint32_t l = uint32_t(__builtin_amdgcn_readlane(int(lo), jj));
+  const uint32_t h = uint32_t(__builtin_amdgcn_readlane(int(hi), jj));
+  return int64_t((uint64_t(h) << 32) | uint64_t(l));
+}
+constexpr int STRIPE = 256;                 // columns per wave
+
+__global__ void __launch_bounds__(GW * 64)
+pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, int64_t ld,
+                   const int32_t* __restrict__ rowmap, const int64_t* __restrict__ indptr,
+                   const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                   int32_t nusers, int64_t col0, int64_t cols, float beta,
+                   float* __restrict__ scores, int64_t score_ld, int32_t* __restrict__ nan_count) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t slot = int64_t(blockIdx.x) * GW + w;
+  if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
+  const int64_t u = users[slot];
+  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  const int64_t x = int64_t(blockIdx.y) * STRIPE + lane * 4;   // column within the block
+  const bool full = x + 4 <= cols;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
+  for (int64_t j0 = 0; j0 < hl; j0 += 64) {
+    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    // row offsets of 64 history items, one per lane, broadcast with readlane below
+    const int64_t mine = lane < jn ? int64_t(rowmap[indices[hb + j0 + lane]]) * ld : 0;
+    const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
+    if (full) {
+#pragma unroll 8
+      for (int jj = 0; jj < jn; ++jj) {
+        const int64_t o = bcast64(mlo, mhi, jj) + x;
+        const nf4 e = load4(E + o);
+        const nf4 t = load4(ES + o);
+        s0 += e.x; s1 += e.y; s2 += e.z; s3 += e.w;
+        n0 += t.x; n1 += t.y; n2 += t.z; n3 += t.w;
+      }
+    } else {
+      for (int jj = 0; jj < jn; ++jj) {
+        const int64_t o = bcast64(mlo, mhi, jj) + x;
+        if (x < cols) { s0 += E[o]; n0 += ES[o]; }
+        if (x + 1 < cols) { s1 += E[o + 1]; n1 += ES[o + 1]; }
+        if (x + 2 < cols) { s2 += E[o + 2]; n2 += ES[o + 2]; }
+      }
+    }
+  }
+  float* out = scores + slot * score_ld + col0 + x;
+  const float S[4] = {s0, s1, s2, s3}, N[4] = {n0, n1, n2, n3};
+  int nan = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (x + q < cols) {
+      float logit = 0.f;   // empty history: logit 0
+      if (hl > 0) logit = N[q] / ((beta == 0.5f) ? sqrtf(S[q]) : powf(S[q], beta));
+      float sc = 1.0f / (1.0f + expf(-logit));
+      if (logit != logit) {
+        sc = __builtin_nanf("");
+        ++nan;
+      }
+      out[q] = sc;
+    }
+  }
+  __threadfence_block();   // this wave's score stores land before its -1 stores below
+  const int64_t lo = col0 + int64_t(blockIdx.y) * STRIPE;
+  const int64_t hi = std::min<int64_t>(lo + STRIPE, col0 + cols);
+  for (int64_t j = lane; j < hl; j += 64) {
+    const int64_t c = indices[hb + j];
+    if (c >= lo && c < hi) {
+      float* o = scores + slot * score_ld + c;
+      if (*o != *o) --nan;   // counted above, but not a candidate
+      *o = -1.f;
+    }
+  }
+  if (nan_count) {
+    for (int o = 32; o > 0; o >>= 1) nan += __shfl_xor(nan, o);
+    if (lane == 0 && nan) atomicAdd(nan_count, nan);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t nais_pair_rows_workspace_size(int64_t num_pois) {
+  if (num_pois <= 0) return 0;
+  return size_t((num_pois + SCAN_THREADS - 1) / SCAN_THREADS) * sizeof(int32_t);
+}
+
+int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                       int32_t num_users, int64_t num_pois, int32_t* rowmap, int64_t* items,
+                       int64_t* num_items, void* workspace, size_t workspace_bytes, void* stream) {
+  if (num_users < 0 || num_pois <= 0) return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (!rowmap || !items || !num_items || (num_users > 0 && (!indptr || !indices || !users)))
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  if (!workspace || workspace_bytes < nais_pair_rows_workspace_size(num_pois))
+    return nais_internal_fail(NAIS_E_WORKSPACE, "workspace too small (nais_pair_rows_workspace_size)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(rowmap, 0, size_t(num_pois) * sizeof(int32_t), st) != hipSuccess)
+    return nais_internal_fail(NAIS_E_HIP, "memset failed");
+  for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_users - u0);
+    hipLaunchKernelGGL(mark_kernel, dim3((unsigned)nb), dim3(256), 0, st, indptr, indices, users + u0,
+                       rowmap);
+  }
+  const int64_t nb = (num_pois + SCAN_THREADS - 1) / SCAN_THREADS;
+  int32_t* bsum = static_cast<int32_t*>(workspace);
+  hipLaunchKernelGGL(count_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, rowmap, num_pois, bsum);
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(SCAN_THREADS), 0, st, bsum, nb, num_items);
+  hipLaunchKernelGGL(place_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, st, rowmap, num_pois,
+                     bsum, items);
+  return nais_internal_check_launch("pair rows");
+}
+
+int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
+                         const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                         int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
+                         int64_t score_ld, int32_t* nan_count, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || score_ld < col0 + cols)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (num_users == 0 || cols == 0) return NAIS_OK;
+  if (!e || !es || !rowmap || !indptr || !indices || !users || !scores)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  if (ld % 4 != 0) return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t stripes = (cols + STRIPE - 1) / STRIPE;
+  if (stripes > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "cols > 65535 * 256");
+  hipLaunchKernelGGL(pair_gather_kernel, dim3((unsigned)((num_users + GW - 1) / GW), (unsigned)stripes),
+                     dim3(GW * 64), 0, st, e, es, ld, rowmap, indptr, indices, users, num_users, col0,
+                     cols, beta, scores, score_ld, nan_count);
+  return nais_internal_check_launch("pair_gather_kernel");
+}
+
+}  // extern "C"

@@ -60,6 +60,10 @@ class _NAISDevice(nn.Module):
     #   "fp32"   exact fp32 MFMA (a k-ordered fmaf chain); "fp16x3_pairsplit" alternative split.
     # nais_forward (the general model.forward path) is always fp32.
     precision = "fp16x3"
+    # full-catalog strategy of catalog.score_topk / the validation drop-ins: "auto" (pair tables
+    # when the users' history entries outnumber their distinct POIs 3:1, else per user),
+    # "direct" or "pairs" (include/nais.h)
+    catalog_strategy = "auto"
 
     def _check_device(self, *tensors):
         dev = self.embed_history.weight.device

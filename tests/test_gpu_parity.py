@@ -123,10 +123,11 @@ def _catalog_kwargs(variant, z):
     return {"region_of": z["region_of"], "coords": z["coords"]}
 
 
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("variant", ["basic", "region", "region_distance", "distance"])
 @pytest.mark.parametrize("tag", ["init", "trained"])
-def test_catalog_golden(variant, tag, precision):
+def test_catalog_golden(variant, tag, precision, strategy):
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
     z = load_golden(f"catalog_{variant}.npz")
     p = params_from(z, tag)
@@ -134,8 +135,8 @@ def test_catalog_golden(variant, tag, precision):
     P, U = int(z["num_pois"]), int(z["num_users"])
     csr = DeviceCSR.from_arrays(z["indptr"], z["indices"], P, torch.device(DEV))
     kw = _catalog_kwargs(variant, z)
-    full = score_catalog(m, csr, range(U), **kw).cpu().numpy()
-    ids, sc = score_topk(m, csr, range(U), 50, **kw)
+    full = score_catalog(m, csr, range(U), strategy=strategy, **kw).cpu().numpy()
+    ids, sc = score_topk(m, csr, range(U), 50, strategy=strategy, **kw)
     ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
     worst = 0.0
     for u in range(U):
@@ -190,6 +191,19 @@ def test_validation_dropin_metrics(precision):
     ("distance", 16, 16), ("distance", 64, 64), ("distance", 128, 128),
 ])
 def test_catalog_vs_oracle_shapes(variant, D, H, precision):
+    _catalog_vs_oracle(variant, D, H, precision, "direct")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
+@pytest.mark.parametrize("variant,D,H", [
+    ("basic", 16, 16), ("basic", 64, 64), ("basic", 128, 128), ("region", 64, 64),
+    ("region_distance", 64, 64), ("distance", 64, 64),
+])
+def test_catalog_pairs_vs_oracle_shapes(variant, D, H, precision):
+    _catalog_vs_oracle(variant, D, H, precision, "pairs")
+
+
+def _catalog_vs_oracle(variant, D, H, precision, strategy):
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
     P = 1500
@@ -204,8 +218,8 @@ def test_catalog_vs_oracle_shapes(variant, D, H, precision):
         coords = coords.mean(0) + (coords - coords.mean(0)) * 0.01
     if variant in ("region_distance", "distance"):
         kw["coords"] = coords
-    full = score_catalog(m, csr, range(6), **kw).cpu().numpy()
-    ids, sc = score_topk(m, csr, range(6), 50, **kw)
+    full = score_catalog(m, csr, range(6), strategy=strategy, **kw).cpu().numpy()
+    ids, sc = score_topk(m, csr, range(6), 50, strategy=strategy, **kw)
     ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
     for u in range(6):
         h = data.history(u)
