@@ -2,15 +2,20 @@
 """Benchmark: full-catalog NAIS scoring + top-50, scored (user, POI) pairs/s (BASELINE.json metric).
 
 Workload (BASELINE.json configs[3], the "100k POIs" metric config): synthetic Gowalla-scale
-check-ins, 50k users x 100k POIs, d = H = 64, h_u ~ U{1..200}, k = 50, NAIS_basic, fp32.
-A step = one batch of `--users-per-step` users per GPU: every catalog POI is scored against the
-user's whole history by the fused HIP kernel (nais_score_catalog), then a per-user radix-select
-top-50 (nais_topk_rows), then (N > 1) the per-step top-k lists are all-gathered over RCCL.
+check-ins, 50k users x 100k POIs, d = H = 64, h_u ~ U{1..200}, k = 50, NAIS_basic.
 Inputs (tables, CSR, user lists) are resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun); users are sharded across ranks by LPT on the cost
-(P - h_u) * h_u, the POI tables are replicated by an RCCL broadcast from rank 0.
-Per-GPU work per step is fixed -> weak scaling.
+Strategy "pairs" (default for config 4): a step = the WHOLE job -- every user's
+complete catalog scored and its top-50 formed. The per-(history POI, candidate) terms are computed
+once (nais_pair_table: the split-fp16 MFMA catalog kernel in table mode), every user's sums are
+gathered from those tables (nais_pair_gather, HBM-bound), then top-50 (nais_topk_rows). N > 1:
+rank r owns POIs [r*P/N, (r+1)*P/N) for all users (tables, gathers, local top-50), then one RCCL
+all-gather of the [users, 50] blocks and a merge (sharding.distributed_topk_pairs) -- the total
+work is fixed as N grows -> strong scaling.
+
+Strategy "direct" (config 5, or --strategy direct): a step = `--users-per-step` users per GPU,
+each user's catalog scored against its whole history by the fused kernel (nais_score_catalog) +
+top-50; users sharded across ranks by LPT, tables replicated (RCCL broadcast) -> weak scaling.
 """
 from __future__ import annotations
 
@@ -57,6 +62,9 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse N>1 on one GPU")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "pairs", "direct"],
+                    help="auto: pairs for config 4 (each (item, candidate) pair shared by ~50 users), "
+                         "direct for config 5's 4096-user subset (sharing ~1)")
     return ap.parse_args()
 
 
@@ -158,6 +166,9 @@ def main():
     model.precision = a.precision
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
     hist_len = data.hist_len()
+    strategy = a.strategy if a.strategy != "auto" else ("pairs" if a.config == 4 else "direct")
+    if strategy == "pairs":
+        return bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist)
     subset = np.arange(4096) if a.config == 5 else None
     mine = shard_users(hist_len, P, world, users=subset)[rank]
     if a.config == 5:   # the fixed 4096-user subset is the whole timed job: steps cover it once
@@ -307,6 +318,135 @@ def main():
                 "algorithmic_flop_per_launch": flops,
                 "avg_launch_ms": avg_score_s * 1e3,
                 "topk_avg_launch_ms": float(np.mean(topk_ms)),
+            },
+            "cpu_baseline": cpu,
+            "fp32_path": fp32_leg,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
+    """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
+    from poi_recommendation_models_amd.sharding import distributed_topk_pairs
+    P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
+    users = np.arange(a.num_users)
+    group = None
+    if world == 1:   # the same code path with a trivial process group is not needed: call direct
+        from poi_recommendation_models_amd.catalog import _score_topk_pairs
+
+        def job(events=None):
+            return _score_topk_pairs(model, csr, users, K, None, None, None, None, force=True,
+                                     events=events)
+    else:
+        def job(events=None):
+            return distributed_topk_pairs(model, csr, users, K, group=group, events=events)
+
+    def run(precision, nwarm, nsteps):
+        model.precision = precision
+        for _ in range(nwarm):
+            job()
+        evs = [[] for _ in range(nsteps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(nsteps):
+            job(evs[i])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        per = {}
+        for step_ev in evs:
+            for kind, e0, e1 in step_ev:
+                per.setdefault(kind, []).append(e0.elapsed_time(e1))
+        return el, per
+
+    elapsed, per = run(a.precision, a.warmup, a.steps)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pairs_job = float((P - hist_len[users]).sum())            # every user's whole catalog
+    S = (P + world - 1) // world
+    c0, c1 = min(rank * S, P), min((rank + 1) * S, P)
+    NC = c1 - c0
+    entries = int(hist_len.sum())
+    J = int(np.count_nonzero(np.bincount(data.indices, minlength=P)))
+    # algorithmic work per step on this rank
+    gather_bytes = entries * NC * 8 + a.num_users * NC * 4 + entries * 12   # table rows, scores, ids
+    flop_per_pair_item = 2 * D * H + 3 * H + 4 * D                          # SURVEY.md 8(d)
+    table_flops = J * NC * flop_per_pair_item
+    g_ms = sum(per.get("gather", [])) / a.steps
+    t_ms = sum(per.get("table", [])) / a.steps
+    k_ms = sum(per.get("topk", [])) / a.steps
+    n_gl = max(1, len(per.get("gather", [])) // a.steps)
+    achieved = gather_bytes / (g_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        tj = json.load(open(a.traffic_json)).get("pairs_gather", {})
+        if tj.get("num_users") == a.num_users and tj.get("num_pois") == P and tj.get("world") == world:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    fp32_leg = None
+    if world == 1 and not a.no_fp32_leg and a.precision != "fp32":
+        el32, per32 = run("fp32", 0, 1)
+        t32 = sum(per32.get("table", []))
+        fp32_leg = {"precision": "fp32 (v_mfma_f32_32x32x2_f32 tables, exact fp32)", "value": pairs_job / el32,
+                    "unit": "pairs/s", "steps": 1, "table_ms": t32,
+                    "table_tflops": table_flops / (t32 * 1e-3) / 1e12, "peak": PEAK_FP32_MFMA_TFLOPS}
+        model.precision = a.precision
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            rng = np.random.default_rng(100)
+            cpu = cpu_baseline(p_host, data, rng.choice(users, 64, replace=False), K, a.cpu_seconds)
+        out = {
+            "metric": "scored (user,POI) pairs/sec full-catalog + top-50, 100k POIs",
+            "value": pairs_job * a.steps / elapsed,
+            "unit": "pairs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32" if a.precision == "fp32" else
+                     "fp32 (W1 x products as 3 fp16 MFMA products of power-of-two-scaled hi/lo splits, fp32 accumulate)",
+            "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
+            "config": {
+                "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
+                            "score + top-%d; one step = every user's whole catalog" % (a.num_users, P, D, K),
+                "model": "NAIS_basic", "strategy": "pairs", "num_users": a.num_users, "num_pois": P,
+                "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,
+                "pairs_per_step": pairs_job, "history_entries": entries, "distinct_history_pois": J,
+                "parallelism": f"POI columns sharded over {world} GPU(s) (all users per rank), "
+                               "tables replicated, one all-gather + merge of the top-k blocks",
+            },
+            "roofline": {
+                "kernel": "pair_gather_kernel (nais_pair_gather)",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": 8000.0,
+                "unit": "GB/s",
+                "frac": achieved / 8000.0,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": gather_bytes / n_gl,
+                "avg_launch_ms": g_ms / n_gl,
+                "launches_per_step": n_gl,
+                "note": "algorithmic bytes = sum_u h_u x columns x 8 B table reads + score writes; the "
+                        "stripe order lets the Infinity Cache serve part of the reads, so HBM traffic "
+                        "(see traffic) can be below them",
+                "table_kernel": {"name": "catalog_score_x3b_kernel in table mode (nais_pair_table)",
+                                 "bound": "mfma", "ms_per_step": t_ms,
+                                 "achieved_tflops": table_flops / (t_ms * 1e-3) / 1e12 if t_ms else None,
+                                 "peak_tflops": PEAKS[a.precision],
+                                 "frac": (table_flops / (t_ms * 1e-3) / 1e12) / PEAKS[a.precision] if t_ms else None},
+                "topk_ms_per_step": k_ms,
             },
             "cpu_baseline": cpu,
             "fp32_path": fp32_leg,

@@ -208,8 +208,10 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *                      where nais_score_catalog uses the fused split kernel, else exact fp32).
  *   nais_pair_gather   for every user and c in [col0, col0 + cols): N = sum_j es[row(j), c],
  *                      S = sum_j e[row(j), c] over the user's history in CSR order,
- *                      scores[slot*score_ld + c] = sigmoid(N / S^beta) (history POIs = -1, empty
- *                      history = 0.5); NaNs counted into *nan_count as nais_score_catalog does.
+ *                      scores[slot*score_ld + c - score_col0] = sigmoid(N / S^beta) (history
+ *                      POIs = -1, empty history = 0.5; score_col0 = the POI of column 0 of
+ *                      scores, 0 for full rows); NaNs counted into *nan_count as
+ *                      nais_score_catalog does.
  * The caller loops over column blocks sized to its memory budget and runs nais_topk_rows.
  */
 size_t nais_pair_rows_workspace_size(int64_t num_pois);
@@ -223,7 +225,7 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
 int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
                          const int64_t* indptr, const int64_t* indices, const int32_t* users,
                          int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
-                         int64_t score_ld, int32_t* nan_count, void* stream);
+                         int64_t score_ld, int64_t score_col0, int32_t* nan_count, void* stream);
 
 /*
  * New4 family (model.py:1169-1306): the per-POI context tables its forward builds

@@ -131,7 +131,8 @@ def load(path: str | None = None):
     lib.nais_pair_table.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp, vp,
                                     i64, vp]
     lib.nais_pair_gather.restype = i32
-    lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, vp, vp]
+    lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, i64, vp,
+                                     vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

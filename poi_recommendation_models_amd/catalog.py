@@ -187,21 +187,33 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     return ids.to(torch.int64), sc
 
 
+# Column-block width target for the pair tables: narrow enough that the stripe the gather
+# reads stays Infinity-Cache friendly, wide enough that the table launches are efficient
+# (config 4 A/B, profiles/r1/pairs/: 8192 best of 1024 / 8192 / 100000).
+PAIR_BLOCK_COLS = 8192
+
+
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
-                      rows_only=False):
+                      rows_only=False, cols=None, events=None):
+    """Pairs strategy. `cols` = (c0, c1): score only POIs [c0, c1) (top-k ids are global POI ids;
+    a column shard of sharding.distributed_topk_pairs). `events`: optional list that receives
+    (kind, start, end) HIP events around every table / gather / top-k launch."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model.embed_history.weight.shape[0]
     if csr.shape[1] != P:
         raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
+    c0_all, c1_all = cols if cols is not None else (0, P)
+    NC = c1_all - c0_all
     users = np.asarray(list(users), dtype=np.int64)
     n = len(users)
-    if n == 0:
+    if n == 0 or NC <= 0:
         return None
-    if np.any(P - csr.hist_len[users] < k):
+    if cols is None and np.any(P - csr.hist_len[users] < k):
         raise RuntimeError("selected index k out of range")       # torch.topk's error
     lib = _capi.load()
     st = stream if stream is not None else _capi.stream_handle(dev)
+    torch_stream = torch.cuda.current_stream(dev)
     u_all = torch.from_numpy(users.astype(np.int32)).to(dev)
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
     prm = model.nais_params()
@@ -209,6 +221,16 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     items = torch.empty(P, dtype=torch.int64, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = _workspace(dev, lib.nais_pair_rows_workspace_size(P))
+
+    def timed(kind, fn):
+        if events is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch_stream)
+        r = fn()
+        e1.record(torch_stream)
+        events.append((kind, e0, e1))
+        return r
 
     def rows(u_dev, m):
         _capi.check(lib.nais_pair_rows(csr.indptr.data_ptr(), csr.indices.data_ptr(), u_dev.data_ptr(),
@@ -222,7 +244,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     free = torch.cuda.mem_get_info(dev)[0]
     budget = int(free * PAIR_MEMORY_FRACTION)
     # users per pass: their score rows take at most half the budget
-    per_pass = n if rows_only else max(1, min(n, (budget // 2) // (4 * P)))
+    per_pass = n if rows_only else max(1, min(n, (budget // 2) // (4 * NC)))
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
     sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -231,33 +253,35 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
-        scores = torch.empty(m, P, dtype=torch.float32, device=dev)
+        scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
         if J > 0:
-            W = (budget // 2) // (8 * J)
-            W = int(min(P, max(256, W // 256 * 256)))
+            W = min(PAIR_BLOCK_COLS, (budget // 2) // (8 * J))
+            W = int(min(NC, max(256, W // 256 * 256)))
             tab = torch.empty(2, J, W, dtype=torch.float32, device=dev)
-            for c0 in range(0, P, W):
-                cols = min(W, P - c0)
-                _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, cols, _capi.ptr(reg),
-                                                _capi.ptr(cor), _capi.ptr(llm), tab[0].data_ptr(),
-                                                tab[1].data_ptr(), W, st), "nais_pair_table")
-                _capi.check(lib.nais_pair_gather(tab[0].data_ptr(), tab[1].data_ptr(), W,
-                                                 rowmap.data_ptr(), csr.indptr.data_ptr(),
-                                                 csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, cols,
-                                                 float(model.beta), scores.data_ptr(), P,
-                                                 counters[0:1].data_ptr(), st), "nais_pair_gather")
+            for c0 in range(c0_all, c1_all, W):
+                w = min(W, c1_all - c0)
+                timed("table", lambda: _capi.check(lib.nais_pair_table(
+                    prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
+                    tab[0].data_ptr(), tab[1].data_ptr(), W, st), "nais_pair_table"))
+                timed("gather", lambda: _capi.check(lib.nais_pair_gather(
+                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
+                    scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), st), "nais_pair_gather"))
             del tab
         else:
             scores.fill_(0.5)   # every listed user has an empty history: logit 0 (model.py:79-88)
         if rows_only:
             model._last_nan = counters[0:1]
             return scores
-        _capi.check(lib.nais_topk_rows(scores.data_ptr(), P, P, m, k, ids_out[b0:b0 + m].data_ptr(),
-                                       sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(), st),
-                    "nais_topk_rows")
+        timed("topk", lambda: _capi.check(lib.nais_topk_rows(
+            scores.data_ptr(), NC, NC, m, k, ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(),
+            counters[1:2].data_ptr(), st), "nais_topk_rows"))
         del scores
     model._last_nan = counters[0:1]
-    return ids_out.to(torch.int64), sc_out
+    ids = ids_out.to(torch.int64)
+    if c0_all:
+        ids = torch.where(ids >= 0, ids + c0_all, ids)
+    return ids, sc_out
 
 
 def prior_rows(train_matrix, users, a, b, coords, device):

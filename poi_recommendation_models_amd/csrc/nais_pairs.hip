@@ -131,7 +131,8 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
                    const int32_t* __restrict__ rowmap, const int64_t* __restrict__ indptr,
                    const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                    int32_t nusers, int64_t col0, int64_t cols, float beta,
-                   float* __restrict__ scores, int64_t score_ld, int32_t* __restrict__ nan_count) {
+                   float* __restrict__ scores, int64_t score_ld, int64_t score_col0,
+                   int32_t* __restrict__ nan_count) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t slot = int64_t(blockIdx.x) * GW + w;
   if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
@@ -163,7 +164,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
       }
     }
   }
-  float* out = scores + slot * score_ld + col0 + x;
+  float* out = scores + slot * score_ld + (col0 - score_col0) + x;
   const float S[4] = {s0, s1, s2, s3}, N[4] = {n0, n1, n2, n3};
   int nan = 0;
 #pragma unroll
@@ -185,7 +186,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
   for (int64_t j = lane; j < hl; j += 64) {
     const int64_t c = indices[hb + j];
     if (c >= lo && c < hi) {
-      float* o = scores + slot * score_ld + c;
+      float* o = scores + slot * score_ld + (c - score_col0);
       if (*o != *o) --nan;   // counted above, but not a candidate
       *o = -1.f;
     }
@@ -233,8 +234,9 @@ int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int3
 int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
                          const int64_t* indptr, const int64_t* indices, const int32_t* users,
                          int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
-                         int64_t score_ld, int32_t* nan_count, void* stream) {
-  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || score_ld < col0 + cols)
+                         int64_t score_ld, int64_t score_col0, int32_t* nan_count, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || col0 < score_col0 ||
+      score_ld < col0 - score_col0 + cols)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
   if (num_users == 0 || cols == 0) return NAIS_OK;
   if (!e || !es || !rowmap || !indptr || !indices || !users || !scores)
@@ -245,7 +247,7 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
   if (stripes > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "cols > 65535 * 256");
   hipLaunchKernelGGL(pair_gather_kernel, dim3((unsigned)((num_users + GW - 1) / GW), (unsigned)stripes),
                      dim3(GW * 64), 0, st, e, es, ld, rowmap, indptr, indices, users, num_users, col0,
-                     cols, beta, scores, score_ld, nan_count);
+                     cols, beta, scores, score_ld, score_col0, nan_count);
   return nais_internal_check_launch("pair_gather_kernel");
 }
 

@@ -100,6 +100,58 @@ def NAIS_validation_distributed(model, args, num_users, test_positive, val_posit
     return precision_v, recall_v, hit_v, precision_t, recall_t, hit_t
 
 
+def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=None, **kw):
+    """Column-sharded "pairs" strategy: rank r scores every listed user against POIs
+    [r*S, (r+1)*S) (S = ceil(P / world)) -- the pair tables for its columns, the per-user gathers,
+    a local top-k -- then one all_gather of the [n, k] blocks and a merge by nais_topk_rows over
+    the world*k candidates. Ranks own ascending id ranges, so the merge's (score desc, position
+    asc) order is the global (score desc, POI id asc). Every user needs k candidates in every
+    column block (checked; otherwise raises ValueError -- use the user-sharded path)."""
+    import torch.distributed as dist
+    from . import _capi
+    from .catalog import _score_topk_pairs, device_csr
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = model._check_device()
+    csr = device_csr(train_matrix, dev)
+    P = csr.shape[1]
+    users = np.asarray(list(users), dtype=np.int64)
+    n = len(users)
+    S = (P + world - 1) // world
+    if world > 1 and S - int(csr.hist_len[users].max(initial=0)) < k:
+        raise ValueError("a column block has fewer than k candidates for some user")
+    c0, c1 = min(rank * S, P), min((rank + 1) * S, P)
+    ids, sc = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
+                                kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events)
+    if world == 1:
+        return ids, sc
+    gi = torch.empty(world, n, k, dtype=torch.int64, device=dev)
+    gs = torch.empty(world, n, k, dtype=torch.float32, device=dev)
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(gi.unbind(0)), ids.contiguous(), group=group)
+        dist.all_gather(list(gs.unbind(0)), sc.contiguous(), group=group)
+    else:
+        dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
+        dist.all_gather_into_tensor(gs, sc.contiguous(), group=group)
+    return merge_topk(gi, gs, k)
+
+
+def merge_topk(ids, scores, k):
+    """[world, n, k] per-column-block top-k lists (blocks in ascending POI-id order) -> the [n, k]
+    global top-k, (score desc, POI id asc), with nais_topk_rows over the world*k candidates."""
+    from . import _capi
+    world, n, _ = ids.shape
+    dev = ids.device
+    cand_s = scores.permute(1, 0, 2).reshape(n, world * k).contiguous()
+    cand_i = ids.permute(1, 0, 2).reshape(n, world * k)
+    pos = torch.empty(n, k, dtype=torch.int32, device=dev)
+    top = torch.empty(n, k, dtype=torch.float32, device=dev)
+    short = torch.zeros(1, dtype=torch.int32, device=dev)
+    _capi.check(_capi.load().nais_topk_rows(cand_s.data_ptr(), world * k, world * k, n, k,
+                                            pos.data_ptr(), top.data_ptr(), short.data_ptr(),
+                                            _capi.stream_handle(dev)), "nais_topk_rows (merge)")
+    return torch.gather(cand_i, 1, pos.to(torch.int64)), top
+
+
 def allgather_rows(local_rows, num_rows, group=None):
     """Assemble a [num_rows, d] table from per-rank row blocks: rank r holds
     rows [r*S, (r+1)*S) with S = ceil(num_rows / world) (the last block zero-padded), one

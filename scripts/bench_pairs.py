@@ -88,7 +88,7 @@ def main():
             e[1].record()
             _capi.check(lib.nais_pair_gather(tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(),
                                              csr.indptr.data_ptr(), csr.indices.data_ptr(), users.data_ptr(),
-                                             U, c0, cols, 0.5, scores.data_ptr(), P, ctr.data_ptr(), st),
+                                             U, c0, cols, 0.5, scores.data_ptr(), P, 0, ctr.data_ptr(), st),
                         "gather")
             e[2].record()
             torch.cuda.synchronize()

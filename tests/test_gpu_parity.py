@@ -419,3 +419,23 @@ def test_new4_validation_golden(tag, precision):
             assert np.max(np.abs(mine - z[key])) <= SCORE_ATOL
         assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids[u], sc[u],
                                tie_eps=GPU_TIE_EPS, lookup=dict(zip(cand.tolist(), mine.tolist())))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pairs_column_shards_merge_equal_single(world):
+    """The column-sharded pairs path (sharding.distributed_topk_pairs) in one process: each
+    rank's column block scored in turn, the same merge; bit-identical to the single-GPU result."""
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    from poi_recommendation_models_amd.sharding import merge_topk
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P, D, H, U, k = 3000, 64, 64, 40, 50
+    data = make_checkins(U, P, 60, seed=31)
+    p = init_nais_params(P, D, H, seed=5, emb_std=0.3, bias_std=0.1)
+    m = _model("basic", p, precision="fp16x3")
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+    ref_ids, ref_sc = _score_topk_pairs(m, csr, range(U), k, None, None, None, None, force=True)
+    S = (P + world - 1) // world
+    parts = [_score_topk_pairs(m, csr, range(U), k, None, None, None, None, force=True,
+                               cols=(r * S, min((r + 1) * S, P))) for r in range(world)]
+    ids, sc = merge_topk(torch.stack([q[0] for q in parts]), torch.stack([q[1] for q in parts]), k)
+    assert torch.equal(ids, ref_ids) and torch.equal(sc, ref_sc)
