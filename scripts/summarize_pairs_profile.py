@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Copy a gpu_profile.sh run of the pairs-strategy bench into profiles/<round>/pairs/ and record the
+gather kernel's HBM traffic per launch in profiles/traffic.json ("pairs_gather").
+usage: summarize_pairs_profile.py <prof_dir> <out_dir> <num_users> <num_pois> <world>"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+src, dst, users, P, world = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+os.makedirs(dst, exist_ok=True)
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+rows = []
+for sub in ("pmc_fetch", "pmc_write"):
+    for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
+        n = r["Kernel_Name"]
+        if any(t in n for t in ("pair_gather", "catalog", "topk")):
+            name = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+            rows.append({"kernel": name, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
+                         "value_kb": float(r["Counter_Value"]), "grid": r["Grid_Size"],
+                         "wg": r["Workgroup_Size"], "lds": r["LDS_Block_Size"], "vgpr": r["VGPR_Count"]})
+with open(os.path.join(dst, "pmc_summary.csv"), "w", newline="") as fh:
+    w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
+    w.writeheader()
+    w.writerows(rows)
+out = {}
+for tag, key in (("pair_gather", "pairs_gather"), ("catalog", "pairs_table")):
+    sel = [r for r in rows if tag in r["kernel"]]
+    f = [r["value_kb"] for r in sel if r["counter"] == "FETCH_SIZE"]
+    wr = [r["value_kb"] for r in sel if r["counter"] == "WRITE_SIZE"]
+    if not f or not wr:
+        continue
+    fetch, write = sum(f) / len(f), sum(wr) / len(wr)
+    out[key] = {"kernel": sel[0]["kernel"], "num_users": users, "num_pois": P, "world": world,
+                "dispatches": len(f), "fetch_size_kb": fetch, "write_size_kb": write,
+                "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over the "
+                          "same bench command; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch, averaged "
+                          "over the kernel's dispatches (MI355X_MICROARCH.md gfx950 correction)",
+                "source": src}
+tjp = "profiles/traffic.json"
+tj = json.load(open(tjp)) if os.path.exists(tjp) else {}
+tj.update(out)
+json.dump(tj, open(tjp, "w"), indent=1)
+print(json.dumps(out, indent=1))
