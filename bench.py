@@ -329,7 +329,14 @@ def main():
 
 def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
+    from poi_recommendation_models_amd import catalog
     from poi_recommendation_models_amd.sharding import distributed_topk_pairs
+    if os.environ.get("NAIS_PAIR_TABLE_CUS"):          # A/B knobs of the table/gather overlap
+        catalog.PAIR_TABLE_CUS = int(os.environ["NAIS_PAIR_TABLE_CUS"])
+    if os.environ.get("NAIS_PAIR_CU_LAYOUT"):
+        catalog.PAIR_CU_LAYOUT = os.environ["NAIS_PAIR_CU_LAYOUT"]
+    if os.environ.get("NAIS_PAIR_BLOCK_COLS"):
+        catalog.PAIR_BLOCK_COLS = int(os.environ["NAIS_PAIR_BLOCK_COLS"])
     P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
     users = np.arange(a.num_users)
     group = None
@@ -379,6 +386,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     gather_bytes = entries * NC * 8 + a.num_users * NC * 4 + entries * 12   # table rows, scores, ids
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     table_flops = J * NC * flop_per_pair_item
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    table_cus = ncu // 2 if catalog.PAIR_TABLE_CUS < 0 else (catalog.PAIR_TABLE_CUS or ncu)
     g_ms = sum(per.get("gather", [])) / a.steps
     t_ms = sum(per.get("table", [])) / a.steps
     k_ms = sum(per.get("topk", [])) / a.steps
@@ -422,6 +431,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
                             "score + top-%d; one step = every user's whole catalog" % (a.num_users, P, D, K),
                 "model": "NAIS_basic", "strategy": "pairs", "num_users": a.num_users, "num_pois": P,
+                "table_cus": catalog.PAIR_TABLE_CUS, "cu_layout": catalog.PAIR_CU_LAYOUT,
+                "block_cols": catalog.PAIR_BLOCK_COLS,
                 "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,
                 "pairs_per_step": pairs_job, "history_entries": entries, "distinct_history_pois": J,
                 "parallelism": f"POI columns sharded over {world} GPU(s) (all users per rank), "
@@ -441,8 +452,13 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "note": "algorithmic bytes = sum_u h_u x columns x 8 B table reads + score writes; the "
                         "stripe order lets the Infinity Cache serve part of the reads, so HBM traffic "
                         "(see traffic) can be below them",
+                "overlap": "tables on CUs [0, %d) and gathers on the other %d, side by side on "
+                           "CU-masked streams (double-buffered tables)" % (table_cus, ncu - table_cus)
+                           if table_cus < ncu else "serial",
                 "table_kernel": {"name": "catalog_score_x3b_kernel in table mode (nais_pair_table)",
-                                 "bound": "mfma", "ms_per_step": t_ms,
+                                 "bound": "mfma", "ms_per_step": t_ms, "cus": table_cus,
+                                 "frac_of_its_cus": (table_flops / (t_ms * 1e-3) / 1e12) /
+                                                    (PEAKS[a.precision] * table_cus / ncu) if t_ms else None,
                                  "achieved_tflops": table_flops / (t_ms * 1e-3) / 1e12 if t_ms else None,
                                  "peak_tflops": PEAKS[a.precision],
                                  "frac": (table_flops / (t_ms * 1e-3) / 1e12) / PEAKS[a.precision] if t_ms else None},

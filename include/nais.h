@@ -228,6 +228,14 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
                          int64_t score_ld, int64_t score_col0, int32_t* nan_count, void* stream);
 
 /*
+ * A stream restricted to the CUs whose bits are set in cu_mask[mask_words] (bit i = CU i), for
+ * running an MFMA-bound and an HBM-bound kernel side by side on disjoint CUs (the pairs strategy's
+ * table / gather overlap). Destroy with nais_stream_destroy.
+ */
+int32_t nais_stream_create_cu_mask(const uint32_t* cu_mask, uint32_t mask_words, void** stream);
+int32_t nais_stream_destroy(void* stream);
+
+/*
  * New4 family (model.py:1169-1306): the per-POI context tables its forward builds
  * from the near-POI lists before NAIS_basic's attention (self_attention, model.py:1272-1295):
  *   ext_history[p] = [embed_history[p] | result_in[p] | result_out[p]]   [P, embed_size]

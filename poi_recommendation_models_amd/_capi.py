@@ -23,7 +23,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
            "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
            "nais_make_train_batch", "nais_new4_tables", "nais_pair_rows_workspace_size",
-           "nais_pair_rows", "nais_pair_table", "nais_pair_gather")
+           "nais_pair_rows", "nais_pair_table", "nais_pair_gather", "nais_stream_create_cu_mask",
+           "nais_stream_destroy")
 
 
 class NaisParams(ctypes.Structure):
@@ -133,6 +134,10 @@ def load(path: str | None = None):
     lib.nais_pair_gather.restype = i32
     lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, i64, vp,
                                      vp]
+    lib.nais_stream_create_cu_mask.restype = i32
+    lib.nais_stream_create_cu_mask.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
+    lib.nais_stream_destroy.restype = i32
+    lib.nais_stream_destroy.argtypes = [vp]
     v = lib.nais_abi_version()
     if v != ABI_VERSION:
         raise NaisError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

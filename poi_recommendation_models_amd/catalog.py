@@ -187,10 +187,49 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     return ids.to(torch.int64), sc
 
 
-# Column-block width target for the pair tables: narrow enough that the stripe the gather
-# reads stays Infinity-Cache friendly, wide enough that the table launches are efficient
-# (config 4 A/B, profiles/r1/pairs/: 8192 best of 1024 / 8192 / 100000).
-PAIR_BLOCK_COLS = 8192
+# Column-block width of the pair tables. Serial (profiles/r1/pairs/): 8192 best of 1024 / 8192 /
+# 100000. Overlapped (below; profiles/r1/overlap/): 1024 / 2048 / 3072 / 4096 / 8192 columns ->
+# 606 / 610 / 619 / 627 / 665 ms per config-4 step (a shorter pipeline fill).
+PAIR_BLOCK_COLS = 2048
+# Table (MFMA-bound) and gather (HBM-bound) phases of consecutive column blocks run side by side
+# on CU-masked streams: tables on CUs [0, PAIR_TABLE_CUS), gathers on the rest (-1 = half the
+# device's CUs, i.e. 4 of the 8 XCDs each; 0 = serial on the caller's stream). Double-buffered
+# tables. Config-4 A/B at 8192 columns (profiles/r1/overlap/): serial 859-874 ms/step; 96 / 112 /
+# 128 / 144 / 160 / 192 table CUs -> 694 / 695 / 665 / 794 / 772 / 1085 ms (splits off XCD
+# boundaries lose; masks that interleave CU ids are not honoured -- both kernels then share
+# every CU).
+PAIR_TABLE_CUS = -1
+PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
+_masked: dict = {}
+
+
+def _masked_streams(dev, table_cus):
+    """(table stream, gather stream) as torch ExternalStreams over disjoint CU masks (cached)."""
+    key = (str(dev), table_cus, PAIR_CU_LAYOUT)
+    hit = _masked.get(key)
+    if hit is not None:
+        return hit
+    n = torch.cuda.get_device_properties(dev).multi_processor_count
+    if PAIR_CU_LAYOUT == "contiguous":
+        mine = set(range(table_cus))
+    else:   # spread over the CU ids evenly
+        mine = {int(i * n / table_cus) for i in range(table_cus)}
+    words = (n + 31) // 32
+    masks = []
+    for sel in (mine, set(range(n)) - mine):
+        m = (ctypes.c_uint32 * words)()
+        for c in sel:
+            m[c // 32] |= 1 << (c % 32)
+        masks.append(m)
+    lib = _capi.load()
+    out = []
+    with torch.cuda.device(dev):
+        for m in masks:
+            h = ctypes.c_void_p()
+            _capi.check(lib.nais_stream_create_cu_mask(m, words, ctypes.byref(h)), "nais_stream_create_cu_mask")
+            out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    _masked[key] = tuple(out)
+    return _masked[key]
 
 
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
@@ -255,11 +294,44 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             J = rows(u_dev, m)
         scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
         if J > 0:
-            W = min(PAIR_BLOCK_COLS, (budget // 2) // (8 * J))
+            W = min(PAIR_BLOCK_COLS, (budget // 4) // (8 * J))
             W = int(min(NC, max(256, W // 256 * 256)))
-            tab = torch.empty(2, J, W, dtype=torch.float32, device=dev)
-            for c0 in range(c0_all, c1_all, W):
+            blocks = list(range(c0_all, c1_all, W))
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            table_cus = ncu // 2 if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS
+            overlap = 0 < table_cus < ncu and len(blocks) > 1 and stream is None
+            tabs = [torch.empty(2, J, W, dtype=torch.float32, device=dev)
+                    for _ in range(2 if overlap else 1)]
+            if overlap:
+                ts, gs = _masked_streams(dev, table_cus)
+                ts.wait_stream(torch_stream)
+                gs.wait_stream(torch_stream)
+                done_g = [None, None]
+            for b, c0 in enumerate(blocks):
                 w = min(W, c1_all - c0)
+                tab = tabs[b % len(tabs)]
+                if overlap:
+                    if done_g[b % 2] is not None:
+                        ts.wait_event(done_g[b % 2])     # buffer free: its gather finished
+                    e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e_t0.record(ts)
+                    _capi.check(lib.nais_pair_table(
+                        prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
+                        tab[0].data_ptr(), tab[1].data_ptr(), W, ts.cuda_stream), "nais_pair_table")
+                    e_t1.record(ts)
+                    gs.wait_event(e_t1)
+                    e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e_g0.record(gs)
+                    _capi.check(lib.nais_pair_gather(
+                        tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                        csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
+                        scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), gs.cuda_stream),
+                        "nais_pair_gather")
+                    e_g1.record(gs)
+                    done_g[b % 2] = e_g1
+                    if events is not None:
+                        events += [("table", e_t0, e_t1), ("gather", e_g0, e_g1)]
+                    continue
                 timed("table", lambda: _capi.check(lib.nais_pair_table(
                     prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
                     tab[0].data_ptr(), tab[1].data_ptr(), W, st), "nais_pair_table"))
@@ -267,7 +339,13 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
                     scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), st), "nais_pair_gather"))
-            del tab
+            if overlap:
+                torch_stream.wait_stream(gs)
+                torch_stream.wait_stream(ts)
+                for t in tabs:      # the allocator must not hand these to the main stream early
+                    t.record_stream(ts)
+                    t.record_stream(gs)
+            del tabs
         else:
             scores.fill_(0.5)   # every listed user has an empty history: logit 0 (model.py:79-88)
         if rows_only:

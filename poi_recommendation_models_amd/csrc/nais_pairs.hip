@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <string>
 
 #include "nais.h"
 #include "nais_internal.h"
@@ -249,6 +250,24 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
                      dim3(GW * 64), 0, st, e, es, ld, rowmap, indptr, indices, users, num_users, col0,
                      cols, beta, scores, score_ld, score_col0, nan_count);
   return nais_internal_check_launch("pair_gather_kernel");
+}
+
+int32_t nais_stream_create_cu_mask(const uint32_t* cu_mask, uint32_t mask_words, void** stream) {
+  if (!cu_mask || !mask_words || !stream) return nais_internal_fail(NAIS_E_INVALID, "bad arguments");
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, mask_words, cu_mask);
+  if (e != hipSuccess)
+    return nais_internal_fail(NAIS_E_HIP, (std::string("hipExtStreamCreateWithCUMask: ") +
+                                           hipGetErrorString(e)).c_str());
+  *stream = s;
+  return NAIS_OK;
+}
+
+int32_t nais_stream_destroy(void* stream) {
+  if (!stream) return NAIS_OK;
+  return hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+             ? NAIS_OK
+             : nais_internal_fail(NAIS_E_HIP, "hipStreamDestroy failed");
 }
 
 }  // extern "C"
