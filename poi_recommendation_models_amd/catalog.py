@@ -203,6 +203,19 @@ PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 _masked: dict = {}
 
 
+def _destroy_masked_streams():
+    """Release the CU-masked streams before interpreter exit: left to the C++ static destructors
+    they outlive the HIP runtime (a crash at exit under rocprofv3)."""
+    if not _masked:
+        return
+    lib = _capi.load()
+    for pair in _masked.values():
+        for s in pair:
+            s.synchronize()
+            lib.nais_stream_destroy(s.cuda_stream)
+    _masked.clear()
+
+
 def _masked_streams(dev, table_cus):
     """(table stream, gather stream) as torch ExternalStreams over disjoint CU masks (cached)."""
     key = (str(dev), table_cus, PAIR_CU_LAYOUT)
@@ -228,6 +241,9 @@ def _masked_streams(dev, table_cus):
             h = ctypes.c_void_p()
             _capi.check(lib.nais_stream_create_cu_mask(m, words, ctypes.byref(h)), "nais_stream_create_cu_mask")
             out.append(torch.cuda.ExternalStream(h.value, device=dev))
+    if not _masked:
+        import atexit
+        atexit.register(_destroy_masked_streams)
     _masked[key] = tuple(out)
     return _masked[key]
 
