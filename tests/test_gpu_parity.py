@@ -439,3 +439,70 @@ def test_pairs_column_shards_merge_equal_single(world):
                                cols=(r * S, min((r + 1) * S, P))) for r in range(world)]
     ids, sc = merge_topk(torch.stack([q[0] for q in parts]), torch.stack([q[1] for q in parts]), k)
     assert torch.equal(ids, ref_ids) and torch.equal(sc, ref_sc)
+
+
+def test_pairs_edge_cases_vs_direct():
+    """Pairs strategy: users with empty histories (0.5 rows) mixed with normal ones, a user whose
+    history covers most of the catalog, duplicate users in the list, region_distance through the
+    reference's latlon_mat; scores equal the direct kernels' within 1e-6 and top-k tie-aware."""
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P = 1200
+    data = make_checkins(10, P, 30, seed=8, num_regions=16, empty_positive_every=3)
+    indptr, indices = list(data.indptr), list(data.indices)
+    big = np.sort(np.random.default_rng(0).choice(P, 1100, replace=False))   # a heavy user
+    indptr2 = np.r_[indptr, indptr[-1] + len(big)]
+    indices2 = np.r_[indices, big]
+    lens = np.diff(indptr2)
+    indptr2[1:4] = indptr2[0]                      # users 0-2: empty histories
+    indptr2[4:] = indptr2[3] + np.cumsum(lens[3:])
+    indices2 = np.concatenate([indices2[:0]] + [np.array(indices[indptr[u]:indptr[u + 1]]) for u in range(3, 10)] + [big])
+    for variant in ("basic", "region_distance"):
+        p = init_nais_params(P, 32, 32, seed=3, emb_std=0.3, variant=variant, num_regions=16,
+                             bias_std=0.1)
+        m = _model(variant, p, precision="fp16x3")
+        csr = DeviceCSR.from_arrays(indptr2, indices2, P, torch.device(DEV))
+        c = data.place_coords
+        kw = {} if variant == "basic" else {"region_of": data.region_of,
+                                            "latlon_mat": np.abs(c[:, None, :] - c[None, :, :])}
+        users = [0, 5, 10, 1, 5, 7]
+        a = score_catalog(m, csr, users, strategy="direct", **kw).cpu().numpy()
+        b = score_catalog(m, csr, users, strategy="pairs", **kw).cpu().numpy()
+        assert np.all(b[0] == 0.5) and np.all(b[3] == 0.5)
+        np.testing.assert_array_equal(a == -1.0, b == -1.0)
+        assert np.max(np.abs(a - b)) <= 1e-6, np.max(np.abs(a - b))
+        ia, sa = score_topk(m, csr, users, 50, strategy="direct", **kw)
+        ib, sb = score_topk(m, csr, users, 50, strategy="pairs", **kw)
+        for r in range(len(users)):
+            assert_topk_equivalent(ia[r].cpu().numpy(), sa[r].cpu().numpy(), ib[r].cpu().numpy(),
+                                   sb[r].cpu().numpy(), tie_eps=GPU_TIE_EPS)
+
+
+def test_pairs_auto_choice_and_new4():
+    """strategy="auto" takes the pairs route only when histories overlap enough; New4 (extended
+    tables) scores identically through both routes."""
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
+    calls = []
+    orig = catalog._score_topk_pairs
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r is not None)
+        return r
+    z = load_golden("new4_catalog.npz")
+    m = _new4(params_from(z, "trained"), "fp16x3")
+    m.extended_tables(z["near"])
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    csr = DeviceCSR.from_arrays(z["indptr"], z["indices"], P, torch.device(DEV))
+    catalog._score_topk_pairs = spy
+    try:
+        ia, sa = score_topk(m, csr, range(U), 50)                       # sharing ~1: direct
+        few = np.repeat(np.arange(U), 8)                                # 8x the same histories
+        ib, sb = score_topk(m, csr, few, 50)                            # sharing 8: pairs
+    finally:
+        catalog._score_topk_pairs = orig
+    assert calls == [False, True]
+    for r, u in enumerate(few):
+        assert_topk_equivalent(ia[u].cpu().numpy(), sa[u].cpu().numpy(), ib[r].cpu().numpy(),
+                               sb[r].cpu().numpy(), tie_eps=GPU_TIE_EPS)
