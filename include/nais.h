@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 5
+#define NAIS_ABI_VERSION 6
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -248,6 +248,70 @@ int32_t nais_new4_tables(const float* embed_history, const float* embed_target,
                          const float* embed_ingoing, const float* embed_outgoing,
                          int64_t num_pois, int32_t embed_size, const int64_t* near_pois,
                          int32_t num_near, float* ext_history, float* ext_target, void* stream);
+
+/*
+ * The near-POI pooling every table-based New4-family member runs (New4 / New4_padding /
+ * all_in_out / transform_ingoing_outgoing / transform_attn: two pools, model.py:1269-1295,
+ * 1551-1566, 1922-1950; nearPOI_embedding / only_area_not_inout: one pool, model.py:1680-1686,
+ * 2198-2218; no_POI_emb: two pools of width embed_size/2, model.py:1797-1812). For every p < P:
+ *   x_k = kv_src[near[p][k]], q = query_src[near[p][0]]              (rows of width dim)
+ *   key_k = wk x_k + bk, val_k = wv x_k + bv, q = wq q + bq         (nn.Linear [dim, dim], [dim];
+ *                                                 NULL weight = identity, NULL bias = zero)
+ *   out[p * out_ld + c] = (softmax(q . reshape(key, [dim, K]) / sqrt(scale_dim)) @ val)[c]
+ * out may point into a column range of a wider row table (out_ld >= dim).
+ * nais_copy_columns: dst[p * dst_ld + dst_col0 + c] = src[p * src_ld + c], p < rows, c < dim.
+ */
+int32_t nais_near_attention(const float* query_src, const float* kv_src, int64_t num_pois,
+                            int32_t dim, const int64_t* near_pois, int32_t num_near,
+                            const float* wq, const float* bq, const float* wk, const float* bk,
+                            const float* wv, const float* bv, float scale_dim, float* out,
+                            int64_t out_ld, void* stream);
+int32_t nais_copy_columns(const float* src, int64_t src_ld, int64_t rows, int32_t dim, float* dst,
+                          int64_t dst_ld, int32_t dst_col0, void* stream);
+
+/*
+ * transform_attn (model.py:1959-2098): dot-product attention over New4-layout rows (SURVEY.md
+ * 8(f4)). Its query/key/value projections act on one POI row each, so they are per-POI tables:
+ *   xh, xt   [P, D]  history / target rows (nais_near_attention + nais_copy_columns, New4 layout)
+ *   qt = xt Wq^T + bq, kh = xh Wk^T + bk, vh = xh Wv^T + bv   [P, D]   (nais_linear_rows)
+ * and the prediction (model.py:2030-2055) is
+ *   logit = sum_j m_j e_j (vh_j . xt_c) / (sum_j m_j e_j)^beta,  e_j = exp(qt_c . kh_j / sqrt(scale_dim))
+ * with m_j = [h_j != c]; scale_dim = embed_size (torch.sqrt(torch.tensor(self.embed_size))).
+ * nais_dot_forward: out[r] for rows r < b as nais_forward (flags, nan_count). For n == 1 it
+ *   restates the reference's shapes exactly: exp_A.squeeze(dim=-1) (model.py:2042) leaves [b] and
+ *   the mask broadcast couples all b rows: out_r = m_r s_r S / (m_r S)^beta, S = sum_r' e_r'.
+ * nais_dot_pair_table: the pair tables of nais_pair_table for this core (E = e_jc, ES = e_jc s_jc),
+ *   consumed by nais_pair_gather unchanged.
+ * nais_dot_single_fixup: for the listed users with exactly one history item, overwrite their score
+ *   rows with new4_validation's chunk-coupled scores (1024-candidate chunks of the ascending
+ *   complement list, validation.py:262-270): score_c = sigmoid(s_c S_k / S_k^beta), S_k the sum of
+ *   e over c's chunk. Columns [col0, col0 + cols) of rows laid out as in nais_pair_gather.
+ * nais_linear_rows: y[r, :dout] = x[r, :din] W^T + b (nn.Linear; b may be NULL), dout <= 256.
+ */
+typedef struct nais_dot_tables {
+  int32_t embed_dim;            /* D (<= 128)                                                 */
+  int64_t num_pois;             /* P                                                          */
+  float beta;                   /* 0.5                                                        */
+  float scale_dim;              /* logits divide by sqrt(scale_dim) (= embed_size)            */
+  const float* xh;              /* [P, D] each                                                */
+  const float* xt;
+  const float* qt;
+  const float* kh;
+  const float* vh;
+} nais_dot_tables_t;
+
+int32_t nais_linear_rows(const float* x, int64_t x_ld, int64_t rows, int32_t din, const float* w,
+                         const float* b, int32_t dout, float* y, int64_t y_ld, void* stream);
+int32_t nais_dot_forward(const nais_dot_tables_t* tables, const int64_t* hist, int64_t b, int64_t n,
+                         int64_t hist_ld, const int64_t* target, float* out, int32_t* nan_count,
+                         int32_t flags, void* stream);
+int32_t nais_dot_pair_table(const nais_dot_tables_t* tables, const int64_t* items, int64_t num_items,
+                            int64_t col0, int64_t cols, float* e, float* es, int64_t ld,
+                            void* stream);
+int32_t nais_dot_single_fixup(const nais_dot_tables_t* tables, const int64_t* indptr,
+                              const int64_t* indices, const int32_t* users, int64_t num_users,
+                              int64_t col0, int64_t cols, float* scores, int64_t score_ld,
+                              int64_t score_col0, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Training step of NAIS_basic on one get_NAIS_batch batch (batches.py:24-50):

@@ -14,6 +14,11 @@ op for op, in the reference's order:
 * `attention_distance`         <- model.py:355-395 (NAIS_distance_Embedding.attention_network)
 * `new4_tables`, `forward_new4` <- model.py:1212-1295 (New4: near-POI self_attention, then the
                                   basic attention over the concatenated rows)
+* `near_pool`, `family_tables`, `forward_family` <- the other table-based New4-family members
+                                  (New4_padding model.py:1308, all_in_out :1447, nearPOI_embedding
+                                  :1578, no_POI_emb :1707, transform_ingoing_outgoing :1822,
+                                  only_area_not_inout :2100, transform_attn :1959 with its
+                                  dot-product core `attention_dot`, model.py:2015-2055)
 * `complement_candidates`      <- batches.py:52-65 (set(range(P)) - set(history), ascending)
 * `catalog_scores_*`           <- validation.py:11-22 / 38-49 / 69-121 (chunked forward over all candidates)
 * `topk_ids`                   <- validation.py:26-27 (torch.topk + id lookup), with the build's
@@ -219,22 +224,80 @@ def _softmax(x):
     return (e / e.sum(axis=-1, keepdims=True, dtype=F32)).astype(F32)
 
 
+def _linear(x, w, b):
+    """nn.Linear: x @ W^T + b (float32)."""
+    if w is None:
+        return x
+    y = np.matmul(x, np.asarray(w, F32).T).astype(F32)
+    return (y + np.asarray(b, F32)).astype(F32) if b is not None else y
+
+
+def near_pool(q_tab, kv_tab, near, scale_dim, lq=(None, None), lk=(None, None), lv=(None, None)):
+    """One self_attention pool (model.py:1281-1286 and its siblings): for every POI p,
+    softmax(q . reshape(key, [d, K]) / sqrt(scale_dim)) @ value with q = Q[near[p][0]],
+    keys/values = KV[near[p]] (through the optional Linear projections of
+    transform_ingoing_outgoing, model.py:1934-1943). Returns [P, d]."""
+    near = np.asarray(near, dtype=np.int64)
+    x = np.asarray(kv_tab, F32)[near]                             # [P, K, d]
+    P, K, d = x.shape
+    q = _linear(np.asarray(q_tab, F32)[near[:, 0]], *lq).reshape(P, 1, d)
+    keys = _linear(x, *lk).reshape(P, d, K)                       # reshape, not transpose
+    vals = _linear(x, *lv)
+    scale = np.sqrt(F32(scale_dim)).astype(F32)                   # torch.sqrt(torch.tensor(E/4 | E/2))
+    return (_softmax(np.matmul(q, keys) / scale) @ vals)[:, 0, :].astype(F32)
+
+
+def _in_out_pools(p, near, d, lin=None):
+    """(result_in, result_out) of the two-pool self_attention: result_out pools embed_outgoing with
+    the query from embed_ingoing, result_in the reverse (model.py:1281-1295)."""
+    ein, eout = p["embed_ingoing.weight"], p["embed_outgoing.weight"]
+    none = (None, None)
+    lq = lk = lv = lvin = none
+    if lin:    # transform_ingoing_outgoing: query/key/value Linear; v_in uses query (model.py:1943)
+        lq, lk, lv = ((p[n + ".weight"], p[n + ".bias"]) for n in ("query", "key", "value"))
+        lvin = lq
+    r_out = near_pool(ein, eout, near, d, lq, lk, lv)
+    r_in = near_pool(eout, ein, near, d, lq, lk, lvin)
+    return r_in, r_out
+
+
+# table-based members of the New4 family: the [P, D] (history rows, target rows) NAIS_basic's
+# attention runs over (each forward's cat(...) calls, model.py lines cited per member)
+NEAR_FAMILY = ("New4", "New4_padding", "all_in_out", "nearPOI_embedding", "no_POI_emb",
+               "transform_ingoing_outgoing", "only_area_not_inout", "transform_attn")
+
+
+def family_tables(model, p, near, embed_size):
+    near = np.asarray(near, dtype=np.int64)
+    P = near.shape[0]
+    cat = lambda *a: np.concatenate([np.asarray(x, F32)[:P] for x in a], -1).astype(F32)  # noqa: E731
+    E = embed_size
+    if model in ("New4", "New4_padding", "transform_ingoing_outgoing", "transform_attn"):
+        # :1212-1236, :1351-1375, :1865-1889, :2002-2026
+        r_in, r_out = _in_out_pools(p, near, E / 4, lin=model == "transform_ingoing_outgoing")
+        return cat(p["embed_history.weight"], r_in, r_out), cat(p["embed_target.weight"], r_out, r_in)
+    if model == "all_in_out":                                             # :1492-1517
+        r_in, r_out = _in_out_pools(p, near, E / 4)
+        a, b = p["embed_history_ingoing.weight"], p["embed_history_outgoing.weight"]
+        return cat(a, b, r_in, r_out), cat(b, a, r_out, r_in)
+    if model == "nearPOI_embedding":                                      # :1622-1647, :1680-1686
+        e = p["embed_near.weight"]
+        r = near_pool(e, e, near, E / 2)
+        a, b = p["embed_history_ingoing.weight"], p["embed_history_outgoing.weight"]
+        return cat(a, b, r), cat(b, a, r)
+    if model == "no_POI_emb":                                             # :1743-1760, :1797-1812
+        r_in, r_out = _in_out_pools(p, near, E / 2)
+        return cat(r_in, r_out), cat(r_out, r_in)
+    if model == "only_area_not_inout":                                    # :2141-2165, :2198-2218
+        e = p["embed_area.weight"]
+        r = near_pool(e, e, near, E / 2)
+        return cat(p["embed_history.weight"], r), cat(p["embed_target.weight"], r)
+    raise ValueError(model)
+
+
 def new4_tables(p, near, embed_size):
     """model.py:1272-1295 + 1215-1222: ([P, D] history rows, [P, D] target rows)."""
-    near = np.asarray(near, dtype=np.int64)
-    ein = p["embed_ingoing.weight"].astype(F32)[near]           # [P, K, d4]
-    eout = p["embed_outgoing.weight"].astype(F32)[near]
-    P, K, d4 = ein.shape
-    scale = np.sqrt(F32(embed_size / 4)).astype(F32)             # torch.sqrt(torch.tensor(E/4))
-    q = ein[:, 0, :].reshape(P, 1, d4)
-    k_out = eout.reshape(P, d4, K)                               # reshape, not transpose
-    result_out = (_softmax(np.matmul(q, k_out) / scale) @ eout)[:, 0, :]
-    q = eout[:, 0, :].reshape(P, 1, d4)
-    k_in = ein.reshape(P, d4, K)
-    result_in = (_softmax(np.matmul(q, k_in) / scale) @ ein)[:, 0, :]
-    xh = np.concatenate([p["embed_history.weight"], result_in, result_out], -1).astype(F32)
-    xt = np.concatenate([p["embed_target.weight"], result_out, result_in], -1).astype(F32)
-    return xh, xt
+    return family_tables("New4", p, near, embed_size)
 
 
 def _with_tables(p, xh, xt):
@@ -248,7 +311,59 @@ def forward_new4(p, near, embed_size, user_history, target_item, beta=0.5):
     return _sigmoid(attention_basic(_with_tables(p, xh, xt), user_history, target_item, beta))
 
 
-def catalog_scores_new4(p, near, embed_size, history, num_pois, beta=0.5):
+def catalog_scores_new4(p, near, embed_size, history, num_pois, beta=0.5, model="New4", chunk=1024):
     """validation.py:254-272 (get_NAIS_batch_test_region candidates, chunked forward)."""
-    xh, xt = new4_tables(p, near, embed_size)
-    return catalog_scores_basic(_with_tables(p, xh, xt), history, num_pois, beta)
+    xh, xt = family_tables(model, p, near, embed_size)
+    if model != "transform_attn":
+        return catalog_scores_basic(_with_tables(p, xh, xt), history, num_pois, beta)
+    # the reference's 1024-row chunks matter here: a one-item history couples the rows of a chunk
+    cand = complement_candidates(history, num_pois)
+    hist = np.asarray(history, dtype=np.int64)
+    out = np.empty(len(cand), dtype=F32)
+    for s in range(0, len(cand), chunk):
+        tg = cand[s:s + chunk]
+        uh = np.broadcast_to(hist, (len(tg), len(hist)))
+        out[s:s + chunk] = _sigmoid(attention_dot(p, xh, xt, uh, tg, embed_size, beta))
+    return cand, out
+
+
+def attention_dot(p, xh, xt, user_history, target_item, embed_size, beta=0.5):
+    """transform_attn.attention_network (model.py:2015-2055): q = query(t), k = key(h_j),
+    v = value(h_j) (nn.Linear over the full rows, Dropout on k = identity in eval),
+    logit_j = sum(q * k_j) / sqrt(E); the same masked, beta-smoothed exp pooling, applied to v;
+    prediction = sum_j w_j (v_j . t).
+
+    Restated with torch's shapes: result2 is already [b, n], so exp_A.squeeze(dim=-1)
+    (model.py:2042) turns a one-item history ([b, 1]) into [b], and `exp_A * mask` then broadcasts
+    to [b, b]: for n == 1 every row's weight sums exp over ALL b rows of the call,
+    pred_r = (v_r . t_r) * mask_r * S / (mask_r * S)^beta with S = sum_r' exp(logit_r')."""
+    history = np.asarray(xh, F32)[user_history]
+    target = np.asarray(xt, F32)[target_item]
+    b = target.shape[0]
+    t3 = target.reshape(b, 1, -1)
+    q = _linear(t3, p["query.weight"], p["query.bias"])
+    k = _linear(history, p["key.weight"], p["key.bias"])
+    v = _linear(history, p["value.weight"], p["value.bias"])
+    r2 = ((q * k).sum(axis=-1, dtype=F32) / np.sqrt(F32(embed_size)).astype(F32)).astype(F32)
+    with np.errstate(over="ignore", invalid="ignore"):
+        exp_a = np.exp(r2).astype(F32)
+        if exp_a.shape[-1] == 1:
+            exp_a = exp_a[..., 0]                                 # squeeze(dim=-1)
+        mask = (user_history != target_item.reshape(-1, 1))
+        exp_a = (exp_a * mask).astype(F32)                        # [b, n] or [b, b]
+        exp_sum = np.power(exp_a.sum(axis=-1, dtype=F32), F32(beta)).astype(F32)
+        attn = (exp_a.T / exp_sum).T.astype(F32).reshape(b, -1, 1)
+        result = (v * attn).astype(F32)
+        pred = np.einsum("bnd,bd->bn", result, target, dtype=F32).sum(axis=-1, dtype=F32)
+    return pred.astype(F32)
+
+
+def family_logits(model, p, xh, xt, user_history, target_item, embed_size, beta=0.5):
+    if model == "transform_attn":
+        return attention_dot(p, xh, xt, user_history, target_item, embed_size, beta)
+    return attention_basic(_with_tables(p, xh, xt), user_history, target_item, beta)
+
+
+def forward_family(model, p, near, embed_size, user_history, target_item, beta=0.5):
+    xh, xt = family_tables(model, p, near, embed_size)
+    return _sigmoid(family_logits(model, p, xh, xt, user_history, target_item, embed_size, beta))

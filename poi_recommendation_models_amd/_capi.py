@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE, VARIANT_DISTANCE = 0, 1, 2, 3
 FLAG_SIGMOID = 1
@@ -24,7 +24,15 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
            "nais_make_train_batch", "nais_new4_tables", "nais_pair_rows_workspace_size",
            "nais_pair_rows", "nais_pair_table", "nais_pair_gather", "nais_stream_create_cu_mask",
-           "nais_stream_destroy")
+           "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
+           "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup")
+
+
+class NaisDotTables(ctypes.Structure):
+    """Mirror of `nais_dot_tables_t` (include/nais.h)."""
+    _fields_ = [("embed_dim", ctypes.c_int32), ("num_pois", ctypes.c_int64), ("beta", ctypes.c_float),
+                ("scale_dim", ctypes.c_float), ("xh", ctypes.c_void_p), ("xt", ctypes.c_void_p),
+                ("qt", ctypes.c_void_p), ("kh", ctypes.c_void_p), ("vh", ctypes.c_void_p)]
 
 
 class NaisParams(ctypes.Structure):
@@ -124,6 +132,20 @@ def load(path: str | None = None):
     lib.nais_make_train_batch.argtypes = [vp, vp, i64, i64, i64, i32, u64, vp, vp, vp, vp, vp]
     lib.nais_new4_tables.restype = i32
     lib.nais_new4_tables.argtypes = [vp, vp, vp, vp, i64, i32, vp, i32, vp, vp, vp]
+    lib.nais_near_attention.restype = i32
+    lib.nais_near_attention.argtypes = [vp, vp, i64, i32, vp, i32, vp, vp, vp, vp, vp, vp,
+                                        ctypes.c_float, vp, i64, vp]
+    lib.nais_linear_rows.restype = i32
+    lib.nais_linear_rows.argtypes = [vp, i64, i64, i32, vp, vp, i32, vp, i64, vp]
+    lib.nais_dot_forward.restype = i32
+    lib.nais_dot_forward.argtypes = [ctypes.POINTER(NaisDotTables), vp, i64, i64, i64, vp, vp, vp, i32, vp]
+    lib.nais_dot_pair_table.restype = i32
+    lib.nais_dot_pair_table.argtypes = [ctypes.POINTER(NaisDotTables), vp, i64, i64, i64, vp, vp, i64, vp]
+    lib.nais_dot_single_fixup.restype = i32
+    lib.nais_dot_single_fixup.argtypes = [ctypes.POINTER(NaisDotTables), vp, vp, vp, i64, i64, i64, vp,
+                                          i64, i64, vp]
+    lib.nais_copy_columns.restype = i32
+    lib.nais_copy_columns.argtypes = [vp, i64, i64, i32, vp, i64, i32, vp]
     lib.nais_pair_rows_workspace_size.restype = sz
     lib.nais_pair_rows_workspace_size.argtypes = [i64]
     lib.nais_pair_rows.restype = i32

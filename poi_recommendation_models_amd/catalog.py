@@ -95,12 +95,12 @@ def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlo
                   strategy="direct"):
     """Full score rows f32 [len(users), P] (history POIs = -1.0), via nais_score_catalog
     (strategy "direct") or the pair tables (strategy "pairs", nais_pair_*)."""
-    if strategy == "pairs":
+    if strategy == "pairs" or model._pairs_only:
         return _score_topk_pairs(model, train_matrix, users, 1, region_of, coords, latlon_mat,
                                  None, force=True, rows_only=True)
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
-    P = model.embed_history.weight.shape[0]
+    P = model._item_tables()[0].shape[0]
     users = np.asarray(list(users), dtype=np.int64)
     u_dev = torch.from_numpy(users.astype(np.int32)).to(dev)
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
@@ -139,13 +139,17 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     strategy = strategy or getattr(model, "catalog_strategy", "auto")
     if strategy not in ("auto", "direct", "pairs"):
         raise ValueError(f"unknown strategy {strategy!r}")
+    if model._pairs_only:
+        if prior is not None:
+            raise NotImplementedError(f"{type(model).__name__}: no power-law prior on its catalog path")
+        strategy = "pairs"
     if strategy != "direct" and prior is None:
         got = _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat,
                                 stream, force=strategy == "pairs")
         if got is not None:
             return got
     csr = device_csr(train_matrix, dev)
-    P = model.embed_history.weight.shape[0]
+    P = model._item_tables()[0].shape[0]
     if csr.shape[1] != P:
         raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
     users = np.asarray(list(users), dtype=np.int64)
@@ -255,7 +259,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     (kind, start, end) HIP events around every table / gather / top-k launch."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
-    P = model.embed_history.weight.shape[0]
+    P = model._item_tables()[0].shape[0]
     if csr.shape[1] != P:
         raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
     c0_all, c1_all = cols if cols is not None else (0, P)
@@ -331,9 +335,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         ts.wait_event(done_g[b % 2])     # buffer free: its gather finished
                     e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e_t0.record(ts)
-                    _capi.check(lib.nais_pair_table(
-                        prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
-                        tab[0].data_ptr(), tab[1].data_ptr(), W, ts.cuda_stream), "nais_pair_table")
+                    model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
+                                      tab[1].data_ptr(), W, ts.cuda_stream)
                     e_t1.record(ts)
                     gs.wait_event(e_t1)
                     e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -348,9 +351,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     if events is not None:
                         events += [("table", e_t0, e_t1), ("gather", e_g0, e_g1)]
                     continue
-                timed("table", lambda: _capi.check(lib.nais_pair_table(
-                    prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
-                    tab[0].data_ptr(), tab[1].data_ptr(), W, st), "nais_pair_table"))
+                timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
+                                                         tab[0].data_ptr(), tab[1].data_ptr(), W, st))
                 timed("gather", lambda: _capi.check(lib.nais_pair_gather(
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
@@ -362,6 +364,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     t.record_stream(ts)
                     t.record_stream(gs)
             del tabs
+            model._pair_fixup(csr, u_dev, m, scores, c0_all, c1_all, st)
         else:
             scores.fill_(0.5)   # every listed user has an empty history: logit 0 (model.py:79-88)
         if rows_only:

@@ -10,6 +10,9 @@ signatures follow the reference:
 * `NAIS_distance_Embedding(item_num, embed_size, hidden_size, beta,
                            region_embed_size, dist_embed_size)`                       model.py:306-408
 * `New4(item_num, embed_size, hidden_size, beta, region_embed_size)`                  model.py:1169-1306
+  and the rest of its family with the same signature: `New4_padding` (:1308), `all_in_out`
+  (:1447), `nearPOI_embedding` (:1578), `no_POI_emb` (:1707), `transform_ingoing_outgoing`
+  (:1822), `transform_attn` (:1959, dot-product core), `only_area_not_inout` (:2100)
 
 `forward` evaluates attention_network + sigmoid on the device in one fused kernel
 (`nais_forward`); there is no CPU path: inputs must live on the ROCm device that holds the
@@ -66,7 +69,7 @@ class _NAISDevice(nn.Module):
     catalog_strategy = "auto"
 
     def _check_device(self, *tensors):
-        dev = self.embed_history.weight.device
+        dev = self.attn_layer1.weight.device
         if dev.type != "cuda":
             raise RuntimeError(f"{type(self).__name__}: the NAIS path runs only on a ROCm device "
                                f"(parameters are on {dev}); move the model with .to('cuda')")
@@ -82,6 +85,17 @@ class _NAISDevice(nn.Module):
         """(embed_history, embed_target) tables the kernels index by POI id."""
         return self.embed_history.weight, self.embed_target.weight
 
+    # catalog hooks of the pairs strategy (catalog._score_topk_pairs): the (item, candidate) table
+    # builder, a post-gather pass over the score rows, and whether the direct kernels apply
+    _pairs_only = False
+
+    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream):
+        _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor),
+                                        _capi.ptr(llm), e, es, ld, stream), "nais_pair_table")
+
+    def _pair_fixup(self, csr, users, m, scores, c0, c1, stream):
+        pass
+
     def nais_params(self) -> _capi.NaisParams:
         """`nais_params_t` view of this module's parameters (device pointers, no copies)."""
         eh, et = self._item_tables()
@@ -92,7 +106,7 @@ class _NAISDevice(nn.Module):
         p.region_dim = self.embed_region.weight.shape[1] if hasattr(self, "embed_region") else 0
         p.hidden = self.attn_layer1.weight.shape[0]
         p.din = self.attn_layer1.weight.shape[1]
-        p.num_pois = self.embed_history.weight.shape[0]
+        p.num_pois = eh.shape[0]
         p.num_regions = self.embed_region.weight.shape[0] if hasattr(self, "embed_region") else 0
         p.beta = float(self.beta)
         p.precision = {"fp32": _capi.PRECISION_FP32, "fp16x3": _capi.PRECISION_FP16X3,
@@ -415,74 +429,327 @@ class NAIS_distance_Embedding(_NAISDevice):
                                  sigmoid=False)
 
 
-class New4(_NAISDevice):
-    """New4 (model.py:1169-1306): NAIS_basic's attention over POI rows extended with context
-    vectors from each POI's near-POI list. forward(history, target, near_pois, target_region)
-    builds the two [P, embed_size] tables on the device (`nais_new4_tables`, once per distinct
-    near_pois array and parameter version) and scores with the basic kernels. Eval only; the
-    unused sub-modules (embed_region, query/key/value, drop) are kept for state_dict parity."""
-    VARIANT = _capi.VARIANT_BASIC
+def _as_near(near_pois, dev, P):
+    near = torch.as_tensor(np.asarray(near_pois) if not torch.is_tensor(near_pois) else near_pois,
+                           dtype=torch.int64).to(dev).contiguous()
+    if near.dim() != 2 or near.shape[0] != P or near.shape[1] < 1:
+        raise ValueError(f"near_pois must be [{P}, K]")
+    return near
 
-    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
-        super().__init__()
+
+class _NearPOIModel(_NAISDevice):
+    """Device path of the table-based New4 family (model.py:1169-2228): each
+    forward(history, target, near_pois, target_region) pools every POI's near-POI list
+    (`nais_near_attention`), lays the pools and embedding columns out as two [P, embed_size] row
+    tables (`nais_copy_columns`) and runs NAIS_basic's attention over them with the basic kernels
+    (fused forward, full-catalog scorer, pair tables). The tables are cached per near_pois array
+    and parameter version. Eval only; sub-modules the forward never reads (embed_region,
+    query/key/value where unused, drop) are kept for state_dict parity.
+
+    Subclasses give `_layout()`: (pools, history columns, target columns), where a pool is
+    (name, query table, key/value table, width, scale_dim, (wq, bq, wk, bk, wv, bv) or None) and a
+    column is a pool name or an embedding weight."""
+    VARIANT = _capi.VARIANT_BASIC
+    _ext = None
+
+    def _layout(self):
+        raise NotImplementedError
+
+    def _emb(self, *names_and_dims):
+        for name, d in names_and_dims:
+            setattr(self, name, nn.Embedding(self.item_num, int(d)))
+
+    def _common(self, item_num, embed_size, hidden_size, beta, proj_dim):
         self.embed_size = embed_size
         self.item_num = item_num
         self.beta = beta
         self.hidden_size = hidden_size
-        self.embed_ingoing = nn.Embedding(item_num, int(embed_size / 4))
-        self.embed_outgoing = nn.Embedding(item_num, int(embed_size / 4))
-        self.embed_history = nn.Embedding(item_num, int(embed_size / 2))
-        self.embed_target = nn.Embedding(item_num, int(embed_size / 2))
-        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
         self.relu = nn.ReLU()
         self.sigmoid = nn.Sigmoid()
         self.loss_func = BCELoss()
         self.softmax = nn.Softmax(dim=-1)
         self.attn_layer1 = nn.Linear(embed_size, hidden_size)
         self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
-        self.query = nn.Linear(int(embed_size / 2), int(embed_size / 2))
-        self.key = nn.Linear(int(embed_size / 2), int(embed_size / 2))
-        self.value = nn.Linear(int(embed_size / 2), int(embed_size / 2))
+        self.query = nn.Linear(int(proj_dim), int(proj_dim))
+        self.key = nn.Linear(int(proj_dim), int(proj_dim))
+        self.value = nn.Linear(int(proj_dim), int(proj_dim))
         self.drop = nn.Dropout()
-        self._init_weight_()
-        self._ext = None
 
-    def _init_weight_(self):                                  # model.py:1197-1209
-        for e in (self.embed_history, self.embed_target, self.embed_region, self.embed_ingoing,
-                  self.embed_outgoing):
-            nn.init.normal_(e.weight, std=0.01)
+    def _init_weight_(self):                                  # e.g. model.py:1197-1209
+        for name, m in self.named_children():
+            if isinstance(m, nn.Embedding):
+                nn.init.normal_(m.weight, std=0.01)
+                if m.padding_idx is not None:
+                    with torch.no_grad():
+                        m.weight[m.padding_idx].fill_(0)
         for m in self.modules():
             if isinstance(m, nn.Linear) and m.bias is not None:
                 m.bias.data.zero_()
 
+    def _build_tables(self, near, xh, xt):
+        lib, st = _capi.load(), _capi.stream_handle(near.device)
+        P, D, K = self.item_num, self.embed_size, near.shape[1]
+        pools, hcols, tcols = self._layout()
+        done = {}
+        for name, qt, kvt, d, sd, lin in pools:
+            out = torch.empty(P, d, device=near.device)
+            ptrs = [None] * 6 if lin is None else [t.data_ptr() for t in lin]
+            _capi.check(lib.nais_near_attention(qt.data_ptr(), kvt.data_ptr(), P, d, near.data_ptr(), K,
+                                                *ptrs, float(sd), out.data_ptr(), d, st),
+                        "nais_near_attention")
+            done[name] = out
+        for dst, cols in ((xh, hcols), (xt, tcols)):
+            c0 = 0
+            for c in cols:
+                src = done[c] if isinstance(c, str) else c
+                _capi.check(lib.nais_copy_columns(src.data_ptr(), src.shape[1], P, src.shape[1],
+                                                  dst.data_ptr(), D, c0, st), "nais_copy_columns")
+                c0 += src.shape[1]
+            if c0 != D:
+                raise AssertionError(f"{type(self).__name__}: row layout width {c0} != {D}")
+        return done
+
     def extended_tables(self, near_pois):
         """([P, D] history rows, [P, D] target rows) for this near-POI array (cached)."""
         dev = self._check_device()
-        near = torch.as_tensor(np.asarray(near_pois) if not torch.is_tensor(near_pois) else near_pois,
-                               dtype=torch.int64).to(dev).contiguous()
-        ws = (self.embed_history.weight, self.embed_target.weight, self.embed_ingoing.weight,
-              self.embed_outgoing.weight)
+        P, D = self.item_num, self.embed_size
+        near = _as_near(near_pois, dev, P)
+        ws = [p for p in self.parameters()]
         key = (near.data_ptr(), tuple(near.shape), tuple((w.data_ptr(), w._version) for w in ws))
         if self._ext is not None and self._ext[0] == key:
             return self._ext[1]
-        P, D = self.item_num, self.embed_size
-        if near.dim() != 2 or near.shape[0] != P:
-            raise ValueError(f"near_pois must be [{P}, K]")
         xh = torch.empty(P, D, device=dev)
         xt = torch.empty(P, D, device=dev)
-        _capi.check(_capi.load().nais_new4_tables(*[w.data_ptr() for w in ws], P, D, near.data_ptr(),
-                                                  near.shape[1], xh.data_ptr(), xt.data_ptr(),
-                                                  _capi.stream_handle(dev)), "nais_new4_tables")
+        self._build_tables(near, xh, xt)
         self._ext = (key, (xh, xt), near)
         return xh, xt
 
     def _item_tables(self):
         if self._ext is None:
-            raise RuntimeError("New4: call extended_tables(near_pois) (or forward) first")
+            raise RuntimeError(f"{type(self).__name__}: call extended_tables(near_pois) (or forward) first")
         return self._ext[1]
 
-    def forward(self, history, target, near_pois, target_region):   # model.py:1212-1222
+    def forward(self, history, target, near_pois, target_region):   # e.g. model.py:1212-1222
         if self.training:
-            raise NotImplementedError("New4: training mode is not implemented on the HIP path")
+            raise NotImplementedError(f"{type(self).__name__}: training mode is not implemented on the HIP path")
         self.extended_tables(near_pois)
         return self._run_forward(history, target)
+
+
+class New4(_NearPOIModel):
+    """New4 (model.py:1169-1306): NAIS_basic's attention over POI rows extended with context
+    vectors from each POI's near-POI list: history rows [E_hist | in | out], target rows
+    [E_tgt | out | in] (model.py:1215-1236), in = pool of embed_ingoing queried by embed_outgoing
+    and out the reverse (self_attention, model.py:1269-1295). Built in one call
+    (`nais_new4_tables`)."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 2)
+        self._emb(("embed_ingoing", embed_size / 4), ("embed_outgoing", embed_size / 4),
+                  ("embed_history", embed_size / 2), ("embed_target", embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self._init_weight_()
+
+    def _build_tables(self, near, xh, xt):
+        ws = (self.embed_history.weight, self.embed_target.weight, self.embed_ingoing.weight,
+              self.embed_outgoing.weight)
+        _capi.check(_capi.load().nais_new4_tables(*[w.data_ptr() for w in ws], self.item_num,
+                                                  self.embed_size, near.data_ptr(), near.shape[1],
+                                                  xh.data_ptr(), xt.data_ptr(),
+                                                  _capi.stream_handle(near.device)), "nais_new4_tables")
+
+
+def _in_out_layout(m, d, lin=None, lin_in=None):
+    """The two pools of New4-style self_attention (model.py:1281-1295): out = pool of
+    embed_outgoing queried by embed_ingoing[near[p][0]], in = the reverse."""
+    ein, eout = m.embed_ingoing.weight, m.embed_outgoing.weight
+    return [("out", ein, eout, int(d), d, lin), ("in", eout, ein, int(d), d, lin_in)]
+
+
+def _lin(*layers):
+    return tuple(t for l in layers for t in (l.weight, l.bias))
+
+
+class New4_padding(_NearPOIModel):
+    """New4_padding (model.py:1308-1445): New4 with (item_num + 1)-row tables, padding_idx=0;
+    the forward is New4's (rows p < item_num of every table are read)."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 2)
+        for name, d in (("embed_ingoing", embed_size / 4), ("embed_outgoing", embed_size / 4),
+                        ("embed_history", embed_size / 2), ("embed_target", embed_size / 2)):
+            setattr(self, name, nn.Embedding(item_num + 1, int(d), padding_idx=0))
+        self.embed_region = nn.Embedding(region_embed_size + 1, int(embed_size / 2), padding_idx=0)
+        self._init_weight_()
+
+    def _layout(self):
+        E = self.embed_size
+        return (_in_out_layout(self, E / 4), [self.embed_history.weight, "in", "out"],
+                [self.embed_target.weight, "out", "in"])
+
+
+class all_in_out(_NearPOIModel):
+    """all_in_out (model.py:1447-1576): no per-role POI embedding; history rows
+    [E_hist_in | E_hist_out | in | out], target rows [E_hist_out | E_hist_in | out | in]
+    (model.py:1510-1517; the target rows read the embed_history_* tables too)."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 2)
+        self._emb(("embed_ingoing", embed_size / 4), ("embed_outgoing", embed_size / 4),
+                  ("embed_history_ingoing", embed_size / 4), ("embed_history_outgoing", embed_size / 4),
+                  ("embed_target_ingoing", embed_size / 4), ("embed_target_outgoing", embed_size / 4))
+        self._init_weight_()
+
+    def _layout(self):
+        a, b = self.embed_history_ingoing.weight, self.embed_history_outgoing.weight
+        return _in_out_layout(self, self.embed_size / 4), [a, b, "in", "out"], [b, a, "out", "in"]
+
+
+class nearPOI_embedding(_NearPOIModel):
+    """nearPOI_embedding (model.py:1578-1705): one pool of embed_near (width embed_size/2,
+    model.py:1680-1686); history rows [E_hist_in | E_hist_out | r], target rows
+    [E_hist_out | E_hist_in | r]."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 2)
+        self._emb(("embed_near", embed_size / 2),
+                  ("embed_history_ingoing", embed_size / 4), ("embed_history_outgoing", embed_size / 4),
+                  ("embed_target_ingoing", embed_size / 4), ("embed_target_outgoing", embed_size / 4))
+        self._init_weight_()
+
+    def _layout(self):
+        e, E = self.embed_near.weight, self.embed_size
+        a, b = self.embed_history_ingoing.weight, self.embed_history_outgoing.weight
+        return [("r", e, e, E // 2, E / 2, None)], [a, b, "r"], [b, a, "r"]
+
+
+class no_POI_emb(_NearPOIModel):
+    """no_POI_emb (model.py:1707-1820): only the two pools, each embed_size/2 wide
+    (model.py:1797-1812); history rows [in | out], target rows [out | in]."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 4)
+        self._emb(("embed_ingoing", embed_size / 2), ("embed_outgoing", embed_size / 2))
+        self._init_weight_()
+
+    def _layout(self):
+        return _in_out_layout(self, self.embed_size / 2), ["in", "out"], ["out", "in"]
+
+
+class transform_ingoing_outgoing(_NearPOIModel):
+    """transform_ingoing_outgoing (model.py:1822-1957): New4 whose pools project through
+    query / key / value (nn.Linear(embed_size/4)); the `in` pool's values go through `query`, as
+    the reference writes it (model.py:1943)."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 4)
+        self._emb(("embed_ingoing", embed_size / 4), ("embed_outgoing", embed_size / 4),
+                  ("embed_history", embed_size / 2), ("embed_target", embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self._init_weight_()
+
+    def _layout(self):
+        lin = _lin(self.query, self.key, self.value)
+        lin_in = _lin(self.query, self.key, self.query)
+        return (_in_out_layout(self, self.embed_size / 4, lin, lin_in),
+                [self.embed_history.weight, "in", "out"], [self.embed_target.weight, "out", "in"])
+
+
+class only_area_not_inout(_NearPOIModel):
+    """only_area_not_inout (model.py:2100-2228): one pool of embed_area (embed_size/2,
+    model.py:2198-2218); history rows [E_hist | r], target rows [E_tgt | r]."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size / 2)
+        self._emb(("embed_area", embed_size / 2), ("embed_history", embed_size / 2),
+                  ("embed_target", embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self._init_weight_()
+
+    def _layout(self):
+        e, E = self.embed_area.weight, self.embed_size
+        return ([("r", e, e, E // 2, E / 2, None)], [self.embed_history.weight, "r"],
+                [self.embed_target.weight, "r"])
+
+
+class transform_attn(_NearPOIModel):
+    """transform_attn (model.py:1959-2098): New4's rows, but the NAIS MLP is replaced by a
+    dot-product attention of projected rows (model.py:2030-2033): query/key/value are
+    nn.Linear(embed_size). The projections act on one POI row each, so they run once per table
+    build (`nais_linear_rows`: qt = xt Wq^T + bq, kh = xh Wk^T + bk, vh = xh Wv^T + bv) and the
+    forward / catalog use the dot core (`nais_dot_forward`, `nais_dot_pair_table` + the shared
+    `nais_pair_gather`). One-item histories keep the reference's batch coupling (include/nais.h).
+    The catalog path is always the pairs strategy."""
+    _pairs_only = True
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size):
+        super().__init__()
+        self._common(item_num, embed_size, hidden_size, beta, embed_size)
+        self._emb(("embed_ingoing", embed_size / 4), ("embed_outgoing", embed_size / 4),
+                  ("embed_history", embed_size / 2), ("embed_target", embed_size / 2))
+        self.embed_region = nn.Embedding(region_embed_size, int(embed_size / 2))
+        self._init_weight_()
+
+    def _layout(self):
+        return (_in_out_layout(self, self.embed_size / 4), [self.embed_history.weight, "in", "out"],
+                [self.embed_target.weight, "out", "in"])
+
+    def _build_tables(self, near, xh, xt):
+        super()._build_tables(near, xh, xt)
+        lib, st = _capi.load(), _capi.stream_handle(near.device)
+        P, D = self.item_num, self.embed_size
+        proj = []
+        for src, lin in ((xt, self.query), (xh, self.key), (xh, self.value)):
+            y = torch.empty(P, D, device=near.device)
+            _capi.check(lib.nais_linear_rows(src.data_ptr(), D, P, D, lin.weight.data_ptr(),
+                                             lin.bias.data_ptr(), D, y.data_ptr(), D, st), "nais_linear_rows")
+            proj.append(y)
+        self._proj = proj
+        t = _capi.NaisDotTables()
+        t.embed_dim, t.num_pois, t.beta, t.scale_dim = D, P, float(self.beta), float(D)
+        t.xh, t.xt = xh.data_ptr(), xt.data_ptr()
+        t.qt, t.kh, t.vh = (y.data_ptr() for y in proj)
+        self._dot = t
+
+    def dot_tables(self):
+        """`nais_dot_tables_t` of the current tables (extended_tables must have run)."""
+        self._item_tables()
+        return self._dot
+
+    def forward(self, history, target, near_pois, target_region):   # model.py:2002-2013
+        if self.training:
+            raise NotImplementedError("transform_attn: training mode is not implemented on the HIP path")
+        self.extended_tables(near_pois)
+        dev = self._check_device(history, target)
+        if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
+            raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
+                             f"{tuple(target.shape)}")
+        history = history.to(torch.int64)
+        if history.dim() == 2 and history.shape[1] > 0 and history.stride(1) != 1:
+            history = history.contiguous()
+        target = target.to(torch.int64).contiguous()
+        b, n = history.shape
+        out = torch.empty(b, dtype=torch.float32, device=dev)
+        nan = torch.zeros(1, dtype=torch.int32, device=dev)
+        _capi.check(_capi.load().nais_dot_forward(
+            self._dot, _capi.ptr(history) if n > 0 else None, b, n, history.stride(0) if n > 0 else 0,
+            _capi.ptr(target), out.data_ptr(), nan.data_ptr(), _capi.FLAG_SIGMOID,
+            _capi.stream_handle(dev)), "nais_dot_forward")
+        self._last_nan = nan
+        return out
+
+    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream):
+        _capi.check(lib.nais_dot_pair_table(self.dot_tables(), items.data_ptr(), J, c0, w, e, es, ld, stream),
+                    "nais_dot_pair_table")
+
+    def _pair_fixup(self, csr, users, m, scores, c0, c1, stream):
+        _capi.check(_capi.load().nais_dot_single_fixup(
+            self.dot_tables(), csr.indptr.data_ptr(), csr.indices.data_ptr(), users.data_ptr(), m, c0,
+            c1 - c0, scores.data_ptr(), c1 - c0, c0, stream), "nais_dot_single_fixup")

@@ -82,8 +82,8 @@ def distributed_recommend(model, args, num_users, train_matrix, group=None, **kw
     from .catalog import device_csr, score_topk
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     model.eval()
-    csr = device_csr(train_matrix, model.embed_history.weight.device)
-    P = model.embed_history.weight.shape[0]
+    csr = device_csr(train_matrix, model._check_device())
+    P = model._item_tables()[0].shape[0]
     mine = shard_users(csr.hist_len[:num_users], P, world)[rank]
     ids, sc = score_topk(model, csr, mine, args.topk, **kw)
     ids, sc = gather_topk(mine, ids, sc, num_users, group=group)

@@ -1,0 +1,155 @@
+"""GPU parity of the New4 family beyond New4: New4_padding, all_in_out,
+nearPOI_embedding, no_POI_emb, transform_ingoing_outgoing, only_area_not_inout (near-POI pools
++ the basic kernels) and transform_attn (near-POI pools + the dot-product core), against the
+golden vectors the reference's own classes produced (tests/golden/make_golden_new4_family.py)
+and the CPU oracle. Tolerances as in test_gpu_parity.py (scores within SCORE_ATOL = 1e-4)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from _helpers import SCORE_ATOL, assert_topk_equivalent, load_golden, params_from, positives_from
+from oracle import nais_oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+GPU_TIE_EPS = 1e-6
+TABLE_MEMBERS = ("New4_padding", "all_in_out", "nearPOI_embedding", "no_POI_emb",
+                 "transform_ingoing_outgoing", "only_area_not_inout")
+MEMBERS = TABLE_MEMBERS + ("transform_attn",)
+
+
+def _member(name, p, P, precision="fp32"):
+    from poi_recommendation_models_amd import model as M
+    H, E = p["attn_layer1.weight"].shape
+    R = p["embed_region.weight"].shape[0] if "embed_region.weight" in p else 10
+    if name == "New4_padding":
+        R -= 1
+    m = getattr(M, name)(P, E, H, 0.5, R)
+    sd = m.state_dict()
+    assert set(sd) == set(p), set(sd) ^ set(p)
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(p[k])) for k in sd})
+    m.precision = precision
+    m.report_nan = False
+    return m.to(DEV).eval()
+
+
+def _t(x):
+    return torch.as_tensor(np.ascontiguousarray(x)).to(DEV)
+
+
+@pytest.mark.parametrize("name", MEMBERS)
+def test_family_tables_vs_oracle(name):
+    z = load_golden("new4_family.npz")
+    p = params_from(z, name)
+    m = _member(name, p, 700)
+    xh, xt = m.extended_tables(z["near"])
+    rh, rt = nais_oracle.family_tables(name, p, z["near"], 32)
+    assert np.max(np.abs(xh.cpu().numpy() - rh)) <= 1e-5
+    assert np.max(np.abs(xt.cpu().numpy() - rt)) <= 1e-5
+
+
+@pytest.mark.parametrize("name", MEMBERS)
+@pytest.mark.parametrize("n", [1, 7])
+def test_family_forward_golden(name, n):
+    z = load_golden("new4_family.npz")
+    m = _member(name, params_from(z, name), 700)
+    hist, tgt, ref = (z[f"{name}/n{n}/{k}"] for k in ("hist", "target", "pred"))
+    got = m(_t(hist), _t(tgt), z["near"], _t(np.zeros(len(tgt), np.int64))).cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL
+
+
+class _Args:
+    topk = 50
+
+
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
+@pytest.mark.parametrize("name", MEMBERS)
+def test_family_validation_golden(name, strategy):
+    """new4_validation (validation.py:254-280) with each member: metrics, full score rows of the
+    stored users and tie-aware top-50 against the reference's own run."""
+    from poi_recommendation_models_amd import validation as V
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
+    z = load_golden("new4_family.npz")
+    tag = f"{name}/cat"
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    m = _member(name, params_from(z, tag), P)
+    m.catalog_strategy = strategy
+    X = sp.csr_matrix((np.ones(len(z["indices"])), z["indices"], z["indptr"]), shape=(U, P))
+    got = V.new4_validation(m, _Args(), U, positives_from(z, "test"), positives_from(z, "val"), X,
+                            z["region_of"], [5, 10, 15, 20, 25, 30], z["near_cat"])
+    np.testing.assert_allclose(np.array(got), z[f"{tag}/metrics"], atol=2.0 / U)
+    csr = DeviceCSR.from_arrays(z["indptr"], z["indices"], P, torch.device(DEV))
+    full = score_catalog(m, csr, range(U), strategy=strategy).cpu().numpy()
+    ids, sc = score_topk(m, csr, range(U), 50, strategy=strategy)
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    for u in range(U):
+        hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
+        cand = nais_oracle.complement_candidates(hist, P)
+        mine = full[u][cand]
+        key = f"{tag}/full_scores_u{u}"
+        if key in z.files:
+            assert np.max(np.abs(mine - z[key])) <= SCORE_ATOL
+        assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids[u], sc[u],
+                               tie_eps=GPU_TIE_EPS, lookup=dict(zip(cand.tolist(), mine.tolist())))
+
+
+def test_transform_attn_one_item_histories_golden():
+    """Users with one history item: the reference couples each 1024-candidate chunk
+    (exp_A.squeeze, model.py:2042); nais_dot_single_fixup restates it."""
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
+    z = load_golden("new4_family.npz")
+    pre = "transform_attn/cat1/"
+    indptr, indices = z[pre + "data/indptr"], z[pre + "data/indices"]
+    P, U = int(z[pre + "data/num_pois"]), len(indptr) - 1
+    m = _member("transform_attn", params_from(z, "transform_attn/cat"), P)
+    m.extended_tables(z["near_cat"])
+    csr = DeviceCSR.from_arrays(indptr, indices, P, torch.device(DEV))
+    full = score_catalog(m, csr, range(U)).cpu().numpy()
+    ids, sc = score_topk(m, csr, range(U), 50)
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    assert (np.diff(indptr) == 1).sum() >= 2
+    for u in range(U):
+        cand = nais_oracle.complement_candidates(indices[indptr[u]:indptr[u + 1]], P)
+        mine = full[u][cand]
+        assert np.max(np.abs(mine - z[f"{pre}full_scores_u{u}"])) <= SCORE_ATOL
+        assert_topk_equivalent(z[pre + "topk_ids"][u], z[pre + "topk_scores"][u], ids[u], sc[u],
+                               tie_eps=GPU_TIE_EPS, lookup=dict(zip(cand.tolist(), mine.tolist())))
+
+
+@pytest.mark.parametrize("b", [5, 1024, 2500])
+def test_transform_attn_forward_single_item_batches(b):
+    """n == 1 forward batches larger than one workgroup's 1024 threads, with masked rows
+    (history == target -> NaN), against the oracle's literal restatement of the broadcast."""
+    z = load_golden("new4_family.npz")
+    p = params_from(z, "transform_attn")
+    m = _member("transform_attn", p, 700)
+    rng = np.random.default_rng(b)
+    hist = rng.integers(0, 700, (b, 1)).astype(np.int64)
+    tgt = rng.integers(0, 700, b).astype(np.int64)
+    tgt[::7] = hist[::7, 0]
+    got = m(_t(hist), _t(tgt), z["near"], _t(np.zeros(b, np.int64))).cpu().numpy()
+    ref = nais_oracle.forward_family("transform_attn", p, z["near"], 32, hist, tgt)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL
+    assert int(m._last_nan.item()) == int(np.isnan(ref).sum())
+
+
+@pytest.mark.parametrize("name", ["no_POI_emb", "transform_attn"])
+def test_family_empty_and_ragged_rows(name):
+    """n == 0 (logit 0 -> 0.5) and non-contiguous history views take the same path."""
+    z = load_golden("new4_family.npz")
+    p = params_from(z, name)
+    m = _member(name, p, 700)
+    tgt = np.arange(6, dtype=np.int64)
+    got = m(_t(np.zeros((6, 0), np.int64)), _t(tgt), z["near"], _t(np.zeros(6, np.int64))).cpu().numpy()
+    assert np.all(got == 0.5)
+    wide = np.random.default_rng(0).integers(0, 700, (6, 10)).astype(np.int64)
+    view = _t(wide)[:, 1:8]
+    got = m(view, _t(tgt), z["near"], _t(np.zeros(6, np.int64))).cpu().numpy()
+    ref = nais_oracle.forward_family(name, p, z["near"], 32, wide[:, 1:8], tgt)
+    assert np.max(np.abs(got - ref)) <= SCORE_ATOL

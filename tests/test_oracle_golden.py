@@ -182,3 +182,53 @@ def test_catalog_new4(tag):
         ids, top = nais_oracle.topk_ids(cand, sc, 50)
         assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids, top,
                                tie_eps=ORACLE_TIE_EPS, lookup=dict(zip(cand.tolist(), sc.tolist())))
+
+
+FAMILY = ("New4_padding", "all_in_out", "nearPOI_embedding", "no_POI_emb",
+          "transform_ingoing_outgoing", "transform_attn", "only_area_not_inout")
+
+
+@pytest.mark.parametrize("member", FAMILY)
+@pytest.mark.parametrize("n", [1, 7])
+def test_forward_new4_family(member, n):
+    """The other New4-family members (model.py:1308-2228), run by the reference with .cuda() as
+    the identity (tests/golden/make_golden_new4_family.py)."""
+    z = load_golden("new4_family.npz")
+    p = params_from(z, member)
+    hist, tgt, ref = (z[f"{member}/n{n}/{k}"] for k in ("hist", "target", "pred"))
+    got = nais_oracle.forward_family(member, p, z["near"], 32, hist, tgt)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+
+
+@pytest.mark.parametrize("member", FAMILY)
+def test_catalog_new4_family(member):
+    """new4_validation (validation.py:254-280) with each member."""
+    z = load_golden("new4_family.npz")
+    tag = f"{member}/cat"
+    p = params_from(z, tag)
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    for u in range(U):
+        hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
+        cand, sc = nais_oracle.catalog_scores_new4(p, z["near_cat"], 32, hist, P, model=member)
+        key = f"{tag}/full_scores_u{u}"
+        if key in z.files:
+            np.testing.assert_allclose(sc, z[key], rtol=0, atol=ORACLE_ATOL)
+        ids, top = nais_oracle.topk_ids(cand, sc, 50)
+        assert_topk_equivalent(z[f"{tag}/topk_ids"][u], z[f"{tag}/topk_scores"][u], ids, top,
+                               tie_eps=ORACLE_TIE_EPS, lookup=dict(zip(cand.tolist(), sc.tolist())))
+
+
+def test_catalog_transform_attn_one_item_histories():
+    """transform_attn with 1-item histories: exp_A.squeeze(-1) (model.py:2042) couples the rows of
+    each 1024-candidate chunk of new4_validation; the oracle restates the same chunking."""
+    z = load_golden("new4_family.npz")
+    p = params_from(z, "transform_attn/cat")
+    pre = "transform_attn/cat1/"
+    indptr, indices = z[pre + "data/indptr"], z[pre + "data/indices"]
+    P = int(z[pre + "data/num_pois"])
+    for u in range(len(indptr) - 1):
+        hist = indices[indptr[u]:indptr[u + 1]]
+        cand, sc = nais_oracle.catalog_scores_new4(p, z["near_cat"], 32, hist, P, model="transform_attn")
+        np.testing.assert_allclose(sc, z[f"{pre}full_scores_u{u}"], rtol=0, atol=ORACLE_ATOL)
