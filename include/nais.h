@@ -313,6 +313,46 @@ int32_t nais_dot_single_fixup(const nais_dot_tables_t* tables, const int64_t* in
                               int64_t col0, int64_t cols, float* scores, int64_t score_ld,
                               int64_t score_col0, void* stream);
 
+/*
+ * NAIS_region_distance_disentangled_Embedding (model.py:409-541): two attention
+ * MLPs (POI rows and region rows, both embed_size wide) with a shared additive distance term
+ * d_j = sum_e embed_distance[0][e] * target_distance[r, j]; forward (model.py:446-455) =
+ *   sigmoid( sum_j a_j (h_j . t) + rho_j (g_j . g_t) ),
+ *   a_j = m_j exp(l_j + d_j) / (sum m exp(l + d))^beta, rho_j likewise with the region MLP.
+ * Arguments as nais_forward (regions per entry / per row, target_distance [b, n] f32 with row
+ * stride dist_ld = run.py:326-333's target_dist). Eval arithmetic (the model has no dropout).
+ * nais_pair_distances: out[r * n + j] = f32(powerLaw.dist(coords[target[r]], coords[hist[j]]))
+ *   (haversine km, float64 in the reference's order) -- run.py:326-333 for one batch (one shared
+ *   history of n items, b targets); coords [P, 2] (lat, lng) float64.
+ * The reference's evaluation call for this model (run.py:353) does not match
+ * NAIS_region_distance_validation's signature, so only the forward has a defined meaning.
+ */
+typedef struct nais_disent_params {
+  int32_t embed_dim;            /* D (<= 128)                                                 */
+  int32_t hidden;               /* H (<= 128)                                                 */
+  int64_t num_pois, num_regions;
+  float beta;
+  const float* embed_history;   /* [P, D]                                                     */
+  const float* embed_target;    /* [P, D]                                                     */
+  const float* embed_region;    /* [R, D]                                                     */
+  const float* embed_distance;  /* [dist_embed_size, D] (row 0 is read)                       */
+  const float* w1;              /* attn_layer1 [H, D], [H]; attn_layer2 [1, H]                */
+  const float* b1;
+  const float* w2;
+  const float* region_w1;       /* region_attn_layer1 [H, D], [H]; region_attn_layer2 [1, H]  */
+  const float* region_b1;
+  const float* region_w2;
+} nais_disent_params_t;
+
+int32_t nais_disent_forward(const nais_disent_params_t* params, const int64_t* hist, int64_t b,
+                            int64_t n, int64_t hist_ld, const int64_t* target,
+                            const int64_t* hist_region, int64_t hist_region_ld,
+                            const int64_t* target_region, const float* target_distance,
+                            int64_t dist_ld, float* out, int32_t* nan_count, int32_t flags,
+                            void* stream);
+int32_t nais_pair_distances(const double* coords, const int64_t* hist, int64_t n,
+                            const int64_t* target, int64_t b, float* out, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Training step of NAIS_basic on one get_NAIS_batch batch (batches.py:24-50):
  * b rows (target[b], int64 POI ids) that all share ONE history hist[n] (int64, the user's positives;

@@ -19,6 +19,7 @@ op for op, in the reference's order:
                                   :1578, no_POI_emb :1707, transform_ingoing_outgoing :1822,
                                   only_area_not_inout :2100, transform_attn :1959 with its
                                   dot-product core `attention_dot`, model.py:2015-2055)
+* `attention_disentangled`     <- model.py:457-527 (NAIS_region_distance_disentangled_Embedding)
 * `complement_candidates`      <- batches.py:52-65 (set(range(P)) - set(history), ascending)
 * `catalog_scores_*`           <- validation.py:11-22 / 38-49 / 69-121 (chunked forward over all candidates)
 * `topk_ids`                   <- validation.py:26-27 (torch.topk + id lookup), with the build's
@@ -216,6 +217,38 @@ def catalog_scores_distance(p, history, num_pois, coords, beta=0.5, chunk=2048):
         ll = latlon_pairs(coords, tp, uh).astype(F32)
         out[s:s + chunk] = _sigmoid(attention_distance(p, uh, tg, ll, beta))
     return cand, out
+
+
+def _mlp_logit(x, w1, b1, w2):
+    r1 = np.maximum((x @ np.asarray(w1, F32).T + np.asarray(b1, F32)).astype(F32), F32(0))
+    return (r1 @ np.asarray(w2, F32).reshape(-1, 1))[..., 0].astype(F32)
+
+
+def attention_disentangled(p, user_history, target_item, history_region, target_region,
+                           target_distance, beta=0.5):
+    """NAIS_region_distance_disentangled_Embedding.attention_network (model.py:457-527): an
+    item MLP and a region MLP, both shifted by d_j = sum_e embed_distance[0][e] * dist_j, each
+    normalised with its own beta-smoothed masked exp sum; logits [b]."""
+    history = p["embed_history.weight"][user_history]                # :465
+    hreg = p["embed_region.weight"][history_region]                 # :466
+    target = p["embed_target.weight"][target_item][:, None, :]       # :467, :472
+    treg = p["embed_region.weight"][target_region][:, None, :]       # :468, :473
+    l1 = _mlp_logit((history * target).astype(F32), p["attn_layer1.weight"], p["attn_layer1.bias"],
+                    p["attn_layer2.weight"])                         # :477-478
+    l2 = _mlp_logit((hreg * treg).astype(F32), p["region_attn_layer1.weight"],
+                    p["region_attn_layer1.bias"], p["region_attn_layer2.weight"])   # :480-481
+    wd = p["embed_distance.weight"][0].astype(F32)
+    dist = (wd[None, None, :] * np.asarray(target_distance, F32)[..., None]).sum(-1, dtype=F32)  # :488-491
+    with np.errstate(over="ignore", invalid="ignore"):
+        mask = (user_history != target_item.reshape(-1, 1))
+        e1 = (np.exp((l1 + dist).astype(F32)).astype(F32) * mask).astype(F32)       # :496-502
+        e2 = (np.exp((l2 + dist).astype(F32)).astype(F32) * mask).astype(F32)
+        a1 = (e1.T / np.power(e1.sum(-1, dtype=F32), F32(beta)).astype(F32)).T.astype(F32)   # :504-512
+        a2 = (e2.T / np.power(e2.sum(-1, dtype=F32), F32(beta)).astype(F32)).T.astype(F32)
+        res = np.concatenate([history * a1[..., None], hreg * a2[..., None]], -1).astype(F32)   # :517-520
+        tgt = np.concatenate([target, treg], -1)[:, 0, :]
+        pred = np.einsum("bnd,bd->bn", res, tgt, dtype=F32).sum(-1, dtype=F32)   # :523-524
+    return pred.astype(F32)
 
 
 def _softmax(x):

@@ -25,7 +25,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_make_train_batch", "nais_new4_tables", "nais_pair_rows_workspace_size",
            "nais_pair_rows", "nais_pair_table", "nais_pair_gather", "nais_stream_create_cu_mask",
            "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
-           "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup")
+           "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
+           "nais_disent_forward", "nais_pair_distances")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -33,6 +34,14 @@ class NaisDotTables(ctypes.Structure):
     _fields_ = [("embed_dim", ctypes.c_int32), ("num_pois", ctypes.c_int64), ("beta", ctypes.c_float),
                 ("scale_dim", ctypes.c_float), ("xh", ctypes.c_void_p), ("xt", ctypes.c_void_p),
                 ("qt", ctypes.c_void_p), ("kh", ctypes.c_void_p), ("vh", ctypes.c_void_p)]
+
+
+class NaisDisentParams(ctypes.Structure):
+    """Mirror of `nais_disent_params_t` (include/nais.h)."""
+    _fields_ = [("embed_dim", ctypes.c_int32), ("hidden", ctypes.c_int32), ("num_pois", ctypes.c_int64),
+                ("num_regions", ctypes.c_int64), ("beta", ctypes.c_float)] + \
+        [(n, ctypes.c_void_p) for n in ("embed_history", "embed_target", "embed_region", "embed_distance",
+                                        "w1", "b1", "w2", "region_w1", "region_b1", "region_w2")]
 
 
 class NaisParams(ctypes.Structure):
@@ -144,6 +153,11 @@ def load(path: str | None = None):
     lib.nais_dot_single_fixup.restype = i32
     lib.nais_dot_single_fixup.argtypes = [ctypes.POINTER(NaisDotTables), vp, vp, vp, i64, i64, i64, vp,
                                           i64, i64, vp]
+    lib.nais_disent_forward.restype = i32
+    lib.nais_disent_forward.argtypes = [ctypes.POINTER(NaisDisentParams), vp, i64, i64, i64, vp, vp, i64, vp,
+                                        vp, i64, vp, vp, i32, vp]
+    lib.nais_pair_distances.restype = i32
+    lib.nais_pair_distances.argtypes = [vp, vp, i64, vp, i64, vp, vp]
     lib.nais_copy_columns.restype = i32
     lib.nais_copy_columns.argtypes = [vp, i64, i64, i32, vp, i64, i32, vp]
     lib.nais_pair_rows_workspace_size.restype = sz

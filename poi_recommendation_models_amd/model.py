@@ -9,6 +9,8 @@ signatures follow the reference:
                                   region_embed_size, dist_embed_size)`                model.py:189-304
 * `NAIS_distance_Embedding(item_num, embed_size, hidden_size, beta,
                            region_embed_size, dist_embed_size)`                       model.py:306-408
+* `NAIS_region_distance_disentangled_Embedding(item_num, embed_size, hidden_size, beta,
+                                               region_embed_size, dist_embed_size)`   model.py:409-541
 * `New4(item_num, embed_size, hidden_size, beta, region_embed_size)`                  model.py:1169-1306
   and the rest of its family with the same signature: `New4_padding` (:1308), `all_in_out`
   (:1447), `nearPOI_embedding` (:1578), `no_POI_emb` (:1707), `transform_ingoing_outgoing`
@@ -427,6 +429,100 @@ class NAIS_distance_Embedding(_NAISDevice):
     def attention_network(self, user_history, target_item, target_lat_long_tensor):     # :355-395
         return self._run_forward(user_history, target_item, target_lat_long=target_lat_long_tensor,
                                  sigmoid=False)
+
+
+class NAIS_region_distance_disentangled_Embedding(_NAISDevice):
+    """NAIS_region_distance_disentangled_Embedding (model.py:409-541): an item attention MLP and a
+    region attention MLP (region rows embed_size wide), both shifted by a learned multiple of the
+    target-history distance, normalised separately and summed (`nais_disent_forward`).
+    forward(history, target, history_region, target_region, target_distance) with
+    target_distance [b, n] f32 as run.py:326-333 builds it (`pair_distances` does that on the
+    device). Eval arithmetic; the model has no dropout. The reference's evaluation call for it
+    (run.py:353) does not match NAIS_region_distance_validation, so there is no catalog path."""
+
+    def __init__(self, item_num, embed_size, hidden_size, beta, region_embed_size, dist_embed_size):
+        super().__init__()
+        self.embed_size = embed_size
+        self.item_num = item_num
+        self.beta = beta
+        self.hidden_size = hidden_size
+        self.embed_history = nn.Embedding(item_num, embed_size)
+        self.embed_target = nn.Embedding(item_num, embed_size)
+        self.embed_region = nn.Embedding(region_embed_size, embed_size)
+        self.embed_distance = nn.Embedding(dist_embed_size, embed_size)
+        self.relu = nn.ReLU()
+        self.sigmoid = nn.Sigmoid()
+        self.loss_func = BCELoss()
+        self.attn_layer1 = nn.Linear(embed_size, hidden_size)
+        self.attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self.region_attn_layer1 = nn.Linear(embed_size, hidden_size)
+        self.region_attn_layer2 = nn.Linear(hidden_size, 1, bias=False)
+        self._init_weight_()
+
+    def _init_weight_(self):                                  # model.py:436-444
+        for e in (self.embed_history, self.embed_target, self.embed_region, self.embed_distance):
+            nn.init.normal_(e.weight, std=0.01)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                m.bias.data.zero_()
+
+    def disent_params(self):
+        p = _capi.NaisDisentParams()
+        p.embed_dim, p.hidden = self.embed_size, self.attn_layer1.weight.shape[0]
+        p.num_pois, p.num_regions = self.embed_history.weight.shape[0], self.embed_region.weight.shape[0]
+        p.beta = float(self.beta)
+        for name, t in (("embed_history", self.embed_history.weight), ("embed_target", self.embed_target.weight),
+                        ("embed_region", self.embed_region.weight), ("embed_distance", self.embed_distance.weight),
+                        ("w1", self.attn_layer1.weight), ("b1", self.attn_layer1.bias),
+                        ("w2", self.attn_layer2.weight), ("region_w1", self.region_attn_layer1.weight),
+                        ("region_b1", self.region_attn_layer1.bias), ("region_w2", self.region_attn_layer2.weight)):
+            setattr(p, name, t.data_ptr())
+        return p
+
+    def forward(self, history, target, history_region, target_region, target_distance):   # :446-455
+        if self.training:
+            raise NotImplementedError(f"{type(self).__name__}: training mode is not implemented on the "
+                                      "HIP path; call model.eval()")
+        dev = self._check_device(history, target, history_region, target_region, target_distance)
+        if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
+            raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
+                             f"{tuple(target.shape)}")
+        b, n = history.shape
+        if tuple(history_region.shape) != (b, n) or tuple(target_region.shape) != (b,) or \
+                tuple(target_distance.shape) != (b, n):
+            raise ValueError("history_region and target_distance must be [b, n], target_region [b]")
+
+        def rows(t, dtype):
+            t = t.to(dtype)
+            return t if n == 0 or t.stride(1) == 1 else t.contiguous()
+        history, history_region = rows(history, torch.int64), rows(history_region, torch.int64)
+        td = rows(target_distance, torch.float32)
+        target = target.to(torch.int64).contiguous()
+        target_region = target_region.to(torch.int64).contiguous()
+        out = torch.empty(b, dtype=torch.float32, device=dev)
+        nan = torch.zeros(1, dtype=torch.int32, device=dev)
+        _capi.check(_capi.load().nais_disent_forward(
+            self.disent_params(), _capi.ptr(history) if n else None, b, n, history.stride(0) if n else 0,
+            _capi.ptr(target), _capi.ptr(history_region) if n else None, history_region.stride(0) if n else 0,
+            _capi.ptr(target_region), _capi.ptr(td) if n else None, td.stride(0) if n else 0,
+            out.data_ptr(), nan.data_ptr(), _capi.FLAG_SIGMOID, _capi.stream_handle(dev)),
+            "nais_disent_forward")
+        self._last_nan = nan
+        return out
+
+
+def pair_distances(coords, hist, target):
+    """run.py:326-333 on the device: f32 [b, n] powerLaw.dist (km) between every target and
+    history POI (`nais_pair_distances`). coords: float64 [P, 2] device tensor; hist [n], target [b]."""
+    hist = hist.to(torch.int64).contiguous()
+    target = target.to(torch.int64).contiguous()
+    if coords.dtype != torch.float64 or coords.dim() != 2 or coords.shape[1] != 2 or coords.device.type != "cuda":
+        raise ValueError("coords must be a float64 [P, 2] ROCm tensor")
+    out = torch.empty(target.numel(), hist.numel(), dtype=torch.float32, device=coords.device)
+    _capi.check(_capi.load().nais_pair_distances(coords.contiguous().data_ptr(), _capi.ptr(hist), hist.numel(),
+                                                 _capi.ptr(target), target.numel(), out.data_ptr(),
+                                                 _capi.stream_handle(coords.device)), "nais_pair_distances")
+    return out
 
 
 def _as_near(near_pois, dev, P):

@@ -153,3 +153,64 @@ def test_family_empty_and_ragged_rows(name):
     got = m(view, _t(tgt), z["near"], _t(np.zeros(6, np.int64))).cpu().numpy()
     ref = nais_oracle.forward_family(name, p, z["near"], 32, wide[:, 1:8], tgt)
     assert np.max(np.abs(got - ref)) <= SCORE_ATOL
+
+
+# ------------------------------------------------ NAIS_region_distance_disentangled_Embedding
+def _disent(p):
+    from poi_recommendation_models_amd import model as M
+    P, E = p["embed_history.weight"].shape
+    H = p["attn_layer1.weight"].shape[0]
+    m = M.NAIS_region_distance_disentangled_Embedding(P, E, H, 0.5, p["embed_region.weight"].shape[0],
+                                                      p["embed_distance.weight"].shape[0])
+    sd = m.state_dict()
+    assert set(sd) == set(p)
+    m.load_state_dict({k: torch.from_numpy(np.ascontiguousarray(p[k])) for k in sd})
+    return m.to(DEV).eval()
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 9])
+def test_disentangled_forward_golden(tag, n):
+    from poi_recommendation_models_amd.model import pair_distances
+    z = load_golden("forward_disent.npz")
+    m = _disent(params_from(z, tag))
+    key = f"{tag}/n{n}"
+    hist, tgt, dist, ref = (z[f"{key}/{k}"] for k in ("hist", "target", "dist", "pred"))
+    # run.py:326-333's distances on the device vs the reference's powerLaw.dist: float64 in the
+    # same operation order, but the device sin/cos/acos may differ from glibc's by an ulp, which
+    # can flip the float32 rounding -> within one float32 ulp (2^-23 relative)
+    d_dev = pair_distances(_t(z["coords"]), _t(hist), _t(tgt))
+    np.testing.assert_allclose(d_dev.cpu().numpy(), dist, rtol=2.0 ** -23, atol=0)
+    H2 = np.tile(hist, (len(tgt), 1))
+    ro = z["region_of"]
+    got = m(_t(H2), _t(tgt), _t(ro[H2]), _t(ro[tgt]), d_dev).cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL
+    assert int(m._last_nan.item()) == int(np.isnan(ref).sum())
+
+
+@pytest.mark.parametrize("D,H", [(16, 8), (64, 64), (128, 100)])
+def test_disentangled_shapes_vs_oracle(D, H):
+    """Per-row histories, D / H up to 128 (two hidden units per lane), a strided history view."""
+    rng = np.random.default_rng(D + H)
+    P, R, b, n = 300, 12, 33, 17
+    f = np.float32
+    p = {"embed_history.weight": rng.normal(0, 0.3, (P, D)).astype(f),
+         "embed_target.weight": rng.normal(0, 0.3, (P, D)).astype(f),
+         "embed_region.weight": rng.normal(0, 0.3, (R, D)).astype(f),
+         "embed_distance.weight": rng.normal(0, 0.05, (1, D)).astype(f)}
+    for pre in ("", "region_"):
+        p[pre + "attn_layer1.weight"] = rng.uniform(-D ** -0.5, D ** -0.5, (H, D)).astype(f)
+        p[pre + "attn_layer1.bias"] = rng.normal(0, 0.1, H).astype(f)
+        p[pre + "attn_layer2.weight"] = rng.uniform(-H ** -0.5, H ** -0.5, (1, H)).astype(f)
+    m = _disent(p)
+    wide = rng.integers(0, P, (b, n + 3)).astype(np.int64)
+    hist = wide[:, 2:2 + n]
+    tgt = rng.integers(0, P, b).astype(np.int64)
+    tgt[3] = hist[3, 5]
+    hreg, treg = rng.integers(0, R, (b, n)), rng.integers(0, R, b)
+    dist = rng.uniform(0, 20, (b, n)).astype(f)
+    got = m(_t(wide)[:, 2:2 + n], _t(tgt), _t(hreg), _t(treg), _t(dist)).cpu().numpy()
+    ref = nais_oracle._sigmoid(nais_oracle.attention_disentangled(p, hist, tgt, hreg, treg, dist))
+    assert np.max(np.abs(got - ref)) <= SCORE_ATOL

@@ -232,3 +232,24 @@ def test_catalog_transform_attn_one_item_histories():
         hist = indices[indptr[u]:indptr[u + 1]]
         cand, sc = nais_oracle.catalog_scores_new4(p, z["near_cat"], 32, hist, P, model="transform_attn")
         np.testing.assert_allclose(sc, z[f"{pre}full_scores_u{u}"], rtol=0, atol=ORACLE_ATOL)
+
+
+@pytest.mark.parametrize("tag", ["init", "trained"])
+@pytest.mark.parametrize("n", [1, 9])
+def test_forward_disentangled(tag, n):
+    """NAIS_region_distance_disentangled_Embedding (model.py:409-541) run by the reference, with
+    run.py:326-333's powerLaw.dist distances (tests/golden/make_golden_disent.py)."""
+    from oracle import powerlaw_oracle
+    z = load_golden("forward_disent.npz")
+    p = params_from(z, tag)
+    key = f"{tag}/n{n}"
+    hist, tgt, dist, ref = (z[f"{key}/{k}"] for k in ("hist", "target", "dist", "pred"))
+    H2 = np.tile(hist, (len(tgt), 1))
+    ro = z["region_of"]
+    got = nais_oracle._sigmoid(nais_oracle.attention_disentangled(p, H2, tgt, ro[H2], ro[tgt], dist))
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=ORACLE_ATOL)
+    c = z["coords"]
+    mine = np.array([[powerlaw_oracle.dist(c[a], c[h]) for h in hist] for a in tgt], dtype=np.float32)
+    assert np.array_equal(mine, dist)
