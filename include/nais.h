@@ -359,7 +359,8 @@ int32_t nais_pair_distances(const double* coords, const int64_t* hist, int64_t n
  * the reference repeats it b times, batches.py:30). Replaces, for this batch shape,
  *   prediction = model(user_history, train_data)   (run.py:103; model.py:40-89 in train mode)
  *   loss.backward()                                (run.py:105; BCELoss model.py:21)
- * embed_dim in {8,16,32,64}, hidden <= 64, variant NAIS_VARIANT_BASIC (else NAIS_E_UNSUPPORTED).
+ * NAIS_VARIANT_BASIC; embed_dim / hidden up to 128 (fused MFMA kernels at embed_dim in {8,16,32,64},
+ * hidden <= 64; a general kernel otherwise -- see nais_train_forward_ex for the region variants).
  *
  * Dropout (nn.Dropout(dropout_p), model.py:22,71) keeps hidden unit i of pair (row c, item j) iff
  * a counter hash of (seed, c*n + j, i) is >= dropout_p * 2^32 and scales kept units by 1/(1-p);
@@ -391,6 +392,50 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
 
 int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, float dropout_p,
                           uint8_t* out, void* stream);
+
+/*
+ * The same training forward / backward for every NAIS variant (NAIS_basic, NAIS_regionEmbedding,
+ * NAIS_region_distance_Embedding; run.py:91-280) and any embed_dim / hidden up to 128 (run.py's
+ * defaults are factor_num = hidden_dim = 128). NAIS_basic at embed_dim in {8,16,32,64}, hidden <= 64
+ * runs the fused MFMA kernels above; everything else a general kernel with the same math and the
+ * same dropout draws. The region variants read full rows [embed_history | embed_region[region]]:
+ *   side->hist_region [n], side->target_region [b]  (regions of the history items / target rows,
+ *   get_NAIS_batch_region, batches.py:67-108); region_distance also side->target_lat_long
+ *   [b, n, 2] f32, row stride latlon_ld (run.py:240-245), x100 before dist_layer (model.py:265).
+ * NAIS_region_distance_Embedding has no dropout (model.py:268): pass dropout_p = 0.
+ * Gradients are ADDED into grads (dense, fp32 atomics for repeated ids); embed_region and
+ * dist_w / dist_b are required for the variants that have them. nais_train_forward / _backward
+ * above are these with side = NULL (NAIS_basic only). Workspace: nais_train_workspace_size().
+ */
+typedef struct nais_train_side {
+  const int64_t* hist_region;     /* [n]                                                        */
+  const int64_t* target_region;   /* [b]                                                        */
+  const float* target_lat_long;   /* [b, n, 2] f32 (region_distance)                           */
+  int64_t latlon_ld;              /* row stride of target_lat_long in elements (>= 2n)         */
+} nais_train_side_t;
+
+typedef struct nais_train_grads {
+  float* embed_history;           /* [P, item_dim]  */
+  float* embed_target;            /* [P, item_dim]  */
+  float* embed_region;            /* [R, region_dim] (region variants)                          */
+  float* w1;                      /* [H, din]       */
+  float* b1;                      /* [H]            */
+  float* w2;                      /* [H]            */
+  float* dist_w;                  /* [2, 2] (region_distance)                                   */
+  float* dist_b;                  /* [2]            */
+} nais_train_grads_t;
+
+int32_t nais_train_forward_ex(const nais_params_t* params, const nais_train_side_t* side,
+                              const int64_t* hist, int64_t n, const int64_t* target, int64_t b,
+                              float dropout_p, uint64_t seed, float* pred, float* saved,
+                              int32_t* nan_count, void* workspace, size_t workspace_bytes,
+                              void* stream);
+int32_t nais_train_backward_ex(const nais_params_t* params, const nais_train_side_t* side,
+                               const int64_t* hist, int64_t n, const int64_t* target, int64_t b,
+                               float dropout_p, uint64_t seed, const float* pred,
+                               const float* saved, const float* grad_pred,
+                               const nais_train_grads_t* grads, void* workspace,
+                               size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused training step (run.py:101-109 in one call): forward, BCELoss (model.py:21) added into

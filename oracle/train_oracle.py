@@ -1,4 +1,5 @@
-"""CPU oracle for the NAIS_basic training step -- TEST INFRASTRUCTURE ONLY.
+"""CPU oracle for the NAIS training step (NAIS_basic and the two region variants) -- TEST
+INFRASTRUCTURE ONLY.
 
 Only `tests/`, `__graft_entry__.smoke()` and `bench.py`/`scripts/bench_train.py`'s CPU leg use
 this module; the product package never imports it.
@@ -15,8 +16,9 @@ Restates, in float64 numpy, one step of run.py:101-109 on a get_NAIS_batch batch
                 attn_layer1 and the two embedding gathers (index_add by POI id)
 * adagrad       torch.optim.Adagrad's update (run.py:89)
 
-Pinned against tests/golden/train_step.npz (gradients from the reference's own autograd, dropout
-off); histories may differ per row here (the reference's general [b, n] input).
+Pinned against tests/golden/train_step.npz and train_step_region.npz (gradients from the
+reference's own autograd, dropout off); histories may differ per row here (the reference's
+general [b, n] input).
 """
 from __future__ import annotations
 
@@ -29,6 +31,15 @@ def train_step_basic(p, hist, data, labels, beta=0.5, keep=None, drop_p=0.0):
     """Forward + backward of NAIS_basic. `p`: dict of parameter arrays keyed like the reference's
     state_dict ('embed_history.weight', ...). `keep`: optional [b, n, H] 0/1 dropout mask (the
     kept units are scaled by 1/(1-drop_p)). Returns dict(pred, logit, loss, grads={name: array})."""
+    return train_step(p, hist, data, labels, beta=beta, keep=keep, drop_p=drop_p)
+
+
+def train_step(p, hist, data, labels, hist_region=None, data_region=None, latlon=None, beta=0.5,
+               keep=None, drop_p=0.0):
+    """Forward + backward of NAIS_basic, NAIS_regionEmbedding (model.py:144-180: rows
+    [E_hist | E_reg[region]] against [E_tgt | E_reg[region]], when `hist_region` / `data_region`
+    are given) or NAIS_region_distance_Embedding (model.py:246-297: also the distance feature
+    sigmoid(dist_layer(100 * latlon)) appended to h (.) t, when `latlon` [b, n, 2] is given)."""
     EH = np.asarray(p["embed_history.weight"], F64)
     ET = np.asarray(p["embed_target.weight"], F64)
     W1 = np.asarray(p["attn_layer1.weight"], F64)
@@ -39,10 +50,23 @@ def train_step_basic(p, hist, data, labels, beta=0.5, keep=None, drop_p=0.0):
     y = np.asarray(labels, F64)
     b, n = hist.shape
     H = W1.shape[0]
-
-    h = EH[hist]                                        # model.py:64  [b, n, D]
-    t = ET[data]                                        # model.py:66  [b, D]
+    region = hist_region is not None
+    if region:
+        ER = np.asarray(p["embed_region.weight"], F64)
+        hist_region = np.asarray(hist_region, np.int64)
+        data_region = np.asarray(data_region, np.int64)
+        h = np.concatenate([EH[hist], ER[hist_region]], -1)          # model.py:151-153
+        t = np.concatenate([ET[data], ER[data_region]], -1)          # model.py:155-157
+    else:
+        h = EH[hist]                                    # model.py:64  [b, n, D]
+        t = ET[data]                                    # model.py:66  [b, D]
     x = h * t[:, None, :]                               # model.py:70
+    if latlon is not None:                              # model.py:265-267
+        Wd = np.asarray(p["dist_layer.weight"], F64)
+        bd = np.asarray(p["dist_layer.bias"], F64)
+        ll = np.asarray(latlon, F64) * 100.0
+        feat = 1.0 / (1.0 + np.exp(-(ll @ Wd.T + bd)))   # sigmoid(dist_layer(100 ll))
+        x = np.concatenate([x, feat], -1)
     u = x @ W1.T + b1                                   # model.py:71 attn_layer1
     if keep is not None and drop_p > 0:
         m = np.asarray(keep, F64) * (1.0 / (1.0 - drop_p))   # Dropout (model.py:71)
@@ -81,15 +105,29 @@ def train_step_basic(p, hist, data, labels, beta=0.5, keep=None, drop_p=0.0):
         db1 = du.sum((0, 1))
         dw2 = np.einsum("bn,bnh->h", da, z)
         dx = du @ W1
+        D = h.shape[-1]
+        dfeat = dx[..., D:]
+        dx = dx[..., :D]
         dh = dx * t[:, None, :] + ds[..., None] * t[:, None, :]
         dt = (dx * h).sum(1) + (ds[..., None] * h).sum(1)
+    I = EH.shape[1]
     gEH = np.zeros_like(EH)
-    np.add.at(gEH, hist.reshape(-1), dh.reshape(-1, dh.shape[-1]))
+    np.add.at(gEH, hist.reshape(-1), dh[..., :I].reshape(-1, I))
     gET = np.zeros_like(ET)
-    np.add.at(gET, data, dt)
+    np.add.at(gET, data, dt[:, :I])
     grads = {"embed_history.weight": gEH, "embed_target.weight": gET,
              "attn_layer1.weight": dW1, "attn_layer1.bias": db1,
              "attn_layer2.weight": dw2.reshape(1, -1)}
+    if region:
+        R = ER.shape[1]
+        gER = np.zeros_like(ER)
+        np.add.at(gER, hist_region.reshape(-1), dh[..., I:].reshape(-1, R))
+        np.add.at(gER, data_region, dt[:, I:])
+        grads["embed_region.weight"] = gER
+    if latlon is not None:
+        dpre = dfeat * feat * (1.0 - feat)              # sigmoid backward
+        grads["dist_layer.weight"] = np.einsum("bnk,bnm->km", dpre, ll)
+        grads["dist_layer.bias"] = dpre.sum((0, 1))
     return dict(pred=pred, logit=logit, loss=loss, grads=grads)
 
 

@@ -26,7 +26,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_pair_rows", "nais_pair_table", "nais_pair_gather", "nais_stream_create_cu_mask",
            "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
            "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
-           "nais_disent_forward", "nais_pair_distances")
+           "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
+           "nais_train_backward_ex")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -34,6 +35,18 @@ class NaisDotTables(ctypes.Structure):
     _fields_ = [("embed_dim", ctypes.c_int32), ("num_pois", ctypes.c_int64), ("beta", ctypes.c_float),
                 ("scale_dim", ctypes.c_float), ("xh", ctypes.c_void_p), ("xt", ctypes.c_void_p),
                 ("qt", ctypes.c_void_p), ("kh", ctypes.c_void_p), ("vh", ctypes.c_void_p)]
+
+
+class NaisTrainSide(ctypes.Structure):
+    """Mirror of `nais_train_side_t` (include/nais.h)."""
+    _fields_ = [("hist_region", ctypes.c_void_p), ("target_region", ctypes.c_void_p),
+                ("target_lat_long", ctypes.c_void_p), ("latlon_ld", ctypes.c_int64)]
+
+
+class NaisTrainGrads(ctypes.Structure):
+    """Mirror of `nais_train_grads_t` (include/nais.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("embed_history", "embed_target", "embed_region", "w1",
+                                               "b1", "w2", "dist_w", "dist_b")]
 
 
 class NaisDisentParams(ctypes.Structure):
@@ -153,6 +166,13 @@ def load(path: str | None = None):
     lib.nais_dot_single_fixup.restype = i32
     lib.nais_dot_single_fixup.argtypes = [ctypes.POINTER(NaisDotTables), vp, vp, vp, i64, i64, i64, vp,
                                           i64, i64, vp]
+    lib.nais_train_forward_ex.restype = i32
+    lib.nais_train_forward_ex.argtypes = [ctypes.POINTER(NaisParams), ctypes.POINTER(NaisTrainSide), vp, i64,
+                                          vp, i64, f32, u64, vp, vp, vp, vp, ctypes.c_size_t, vp]
+    lib.nais_train_backward_ex.restype = i32
+    lib.nais_train_backward_ex.argtypes = [ctypes.POINTER(NaisParams), ctypes.POINTER(NaisTrainSide), vp,
+                                           i64, vp, i64, f32, u64, vp, vp, vp,
+                                           ctypes.POINTER(NaisTrainGrads), vp, ctypes.c_size_t, vp]
     lib.nais_disent_forward.restype = i32
     lib.nais_disent_forward.argtypes = [ctypes.POINTER(NaisDisentParams), vp, i64, i64, i64, vp, vp, i64, vp,
                                         vp, i64, vp, vp, i32, vp]

@@ -826,6 +826,288 @@ make_batch_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
+// General training kernels: every NAIS variant (basic, region, region_distance; model.py:8-304)
+// at embed_dim <= 128 (even), hidden <= 128 -- the dims the fused MFMA kernels above do not cover
+// (run.py's defaults are factor_num = hidden_dim = 128) and the region variants' training drivers
+// (run.py:153-200, 222-262). Same math, same dropout hash, same S / N partials + finalize.
+//   full history row hf_j = [embed_history[h_j] | embed_region[hreg_j]]   (region variants)
+//   full target row  tf   = [embed_target[c]    | embed_region[treg_c]]
+//   x = hf_j (.) tf [| sigmoid(dist_layer(100 * latlon_cj))]   (region_distance, model.py:265-267)
+// One wave per batch row (GW rows per workgroup), the slice's items in turn. W1^T sits in LDS with
+// an odd row pitch (H + 1), so the forward (lanes over hidden units) and dx (lanes over dims) both
+// read it conflict-free; x and du are broadcast with readlane in uniform loops. The backward
+// accumulates dW1 / db1 / dw2 / d(dist_layer) and the slice's history-row grads in LDS (ds_add)
+// and adds them to the caller's gradients with global atomics; target-row grads go straight from
+// registers.
+// ---------------------------------------------------------------------------------------------
+constexpr int GW = 8;                 // rows (waves) per workgroup
+constexpr int G_MAX_JS = 32;          // items per slice
+constexpr int G_MAX_D = 128, G_MAX_H = 128, G_MAX_DIN = G_MAX_D + 2;
+
+struct GArgs {
+  const float *eh, *et, *er, *w1, *b1, *w2, *dw, *db;
+  const int64_t *hist, *target, *hreg, *treg;
+  const float* ll;
+  int64_t ll_ld;
+  int64_t b, n;
+  int D, IDIM, RDIM, H, DIN, variant;
+  float beta, dscale;
+  int js;
+  Drop drop;
+};
+
+struct GGrads {
+  float *eh, *et, *er, *w1, *b1, *w2, *dw, *db;
+};
+
+__device__ __forceinline__ float rl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// element d of the full history / target row
+__device__ __forceinline__ float hfull(const GArgs& a, int64_t j, int d) {
+  if (d >= a.D) return 0.f;
+  if (d < a.IDIM) return a.eh[a.hist[j] * a.IDIM + d];
+  return a.er[a.hreg[j] * a.RDIM + (d - a.IDIM)];
+}
+__device__ __forceinline__ float tfull(const GArgs& a, int64_t c, int d) {
+  if (d >= a.D) return 0.f;
+  if (d < a.IDIM) return a.et[a.target[c] * a.IDIM + d];
+  return a.er[a.treg[c] * a.RDIM + (d - a.IDIM)];
+}
+
+struct GPair {
+  float h0, h1, x0, x1;   // hf and x at dims lane, lane + 64
+  float f0, f1;           // distance features x[D], x[D+1] (region_distance), wave-uniform
+  float l0, l1;           // 100 * latlon (region_distance)
+  float v0, v1;           // post-dropout hidden units lane, lane + 64
+  float m0, m1;           // dropout factors
+  float s, a;             // h . t and the attention logit
+};
+
+__device__ __forceinline__ void g_pair_forward(const GArgs& a, const float* W1T, const float* B1,
+                                               const float* W2, int64_t c, int64_t j, float t0,
+                                               float t1, int lane, GPair& p) {
+  const int HP = a.H + 1;
+  p.h0 = hfull(a, j, lane);
+  p.h1 = hfull(a, j, lane + 64);
+  p.x0 = p.h0 * t0;
+  p.x1 = p.h1 * t1;
+  float sp = p.x0 + p.x1;
+  for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o);
+  p.s = sp;
+  p.f0 = p.f1 = p.l0 = p.l1 = 0.f;
+  if (a.variant == NAIS_VARIANT_REGION_DISTANCE) {
+    const float* ll = a.ll + c * a.ll_ld + 2 * j;
+    p.l0 = ll[0] * a.dscale;
+    p.l1 = ll[1] * a.dscale;
+    // sigmoid(dist_layer(100 ll)), model.py:265, in the scorer's operation order
+    p.f0 = 1.0f / (1.0f + expf(-(p.l0 * a.dw[0] + p.l1 * a.dw[1] + a.db[0])));
+    p.f1 = 1.0f / (1.0f + expf(-(p.l0 * a.dw[2] + p.l1 * a.dw[3] + a.db[1])));
+  }
+  const int i0 = lane, i1 = lane + 64;
+  float u0 = i0 < a.H ? B1[i0] : 0.f, u1 = i1 < a.H ? B1[i1] : 0.f;
+  const int dmain = a.D;
+  for (int d = 0; d < dmain; ++d) {
+    const float xd = d < 64 ? rl(p.x0, d) : rl(p.x1, d - 64);
+    u0 = fmaf(W1T[d * HP + i0], xd, u0);
+    if (a.H > 64) u1 = fmaf(W1T[d * HP + i1], xd, u1);
+  }
+  if (a.DIN > a.D) {
+    u0 = fmaf(W1T[a.D * HP + i0], p.f0, u0);
+    u0 = fmaf(W1T[(a.D + 1) * HP + i0], p.f1, u0);
+    if (a.H > 64) {
+      u1 = fmaf(W1T[a.D * HP + i1], p.f0, u1);
+      u1 = fmaf(W1T[(a.D + 1) * HP + i1], p.f1, u1);
+    }
+  }
+  p.m0 = p.m1 = 1.f;
+  if (a.drop.on) {
+    const uint32_t k = a.drop.key(uint32_t(c * a.n + j));
+    p.m0 = a.drop.factor(k, i0);
+    p.m1 = a.drop.factor(k, i1);
+  }
+  p.v0 = i0 < a.H ? u0 * p.m0 : 0.f;
+  p.v1 = i1 < a.H ? u1 * p.m1 : 0.f;
+  float ap = (i0 < a.H ? W2[i0] * fmaxf(p.v0, 0.f) : 0.f);
+  if (i1 < a.H) ap = fmaf(W2[i1], fmaxf(p.v1, 0.f), ap);
+  for (int o = 32; o > 0; o >>= 1) ap += __shfl_xor(ap, o);
+  p.a = ap;
+}
+
+// LDS: W1T [DIN][H+1] | b1 [H] | w2 [H]   (+ backward: dW1 [DIN][H+1] | db1 [H] | dw2 [H] |
+//      d(dist_layer) [8] | dhist [js][D])
+__device__ void g_stage(const GArgs& a, float* L, int tid, int nthreads) {
+  const int HP = a.H + 1;
+  for (int f = tid; f < a.H * a.DIN; f += nthreads) {
+    const int i = f / a.DIN, d = f % a.DIN;
+    L[d * HP + i] = a.w1[f];
+  }
+  float* B1 = L + a.DIN * HP;
+  for (int i = tid; i < a.H; i += nthreads) {
+    B1[i] = a.b1[i];
+    B1[a.H + i] = a.w2[i];
+  }
+}
+
+__global__ void __launch_bounds__(GW * 64)
+g_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
+  extern __shared__ float4 glds4[];
+  float* L = reinterpret_cast<float*>(glds4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t c = int64_t(blockIdx.x) * GW + (tid >> 6);
+  const int64_t j0 = int64_t(blockIdx.y) * a.js;
+  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
+  g_stage(a, L, tid, GW * 64);
+  __syncthreads();
+  if (c >= a.b) return;   // no barriers below
+  const int HP = a.H + 1;
+  const float* W1T = L;
+  const float* B1 = L + a.DIN * HP;
+  const float* W2 = B1 + a.H;
+  const float t0 = tfull(a, c, lane), t1 = tfull(a, c, lane + 64);
+  const int64_t tgt = a.target[c];
+  float S = 0.f, N = 0.f;
+  for (int jj = 0; jj < nj; ++jj) {
+    const int64_t j = j0 + jj;
+    GPair p;
+    g_pair_forward(a, W1T, B1, W2, c, j, t0, t1, lane, p);
+    const float e = expf(p.a) * (a.hist[j] != tgt ? 1.f : 0.f);   // model.py:74-78
+    S += e;
+    N = fmaf(e, p.s, N);
+  }
+  if (lane == 0) {
+    Sp[int64_t(blockIdx.y) * a.b + c] = S;
+    Np[int64_t(blockIdx.y) * a.b + c] = N;
+  }
+}
+
+__global__ void __launch_bounds__(GW * 64)
+g_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
+                  const float* __restrict__ gpred, GGrads g) {
+  extern __shared__ float4 glds4[];
+  float* L = reinterpret_cast<float*>(glds4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int HP = a.H + 1;
+  const int64_t c = int64_t(blockIdx.x) * GW + (tid >> 6);
+  const int64_t j0 = int64_t(blockIdx.y) * a.js;
+  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
+  float* W1T = L;
+  float* B1 = L + a.DIN * HP;
+  float* W2 = B1 + a.H;
+  float* GW1 = W2 + a.H;                 // [DIN][HP]
+  float* GB1 = GW1 + a.DIN * HP;         // [H]
+  float* GW2 = GB1 + a.H;                // [H]
+  float* GDL = GW2 + a.H;                // dist_layer: dw [4] | db [2]   (8 reserved)
+  float* GH = GDL + 8;                   // [js][D]
+  g_stage(a, L, tid, GW * 64);
+  const int acc_n = a.DIN * HP + 2 * a.H + 8 + nj * a.D;
+  for (int f = tid; f < acc_n; f += GW * 64) GW1[f] = 0.f;
+  __syncthreads();
+  if (c < a.b) {
+    const int64_t tgt = a.target[c];
+    const float S = saved[c], N = saved[a.b + c], pc = pred[c];
+    const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid, model.py:55)
+    const float Sb = (a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta);
+    const float dsc = gl / Sb, bn = a.beta * N / S;
+    const float t0 = tfull(a, c, lane), t1 = tfull(a, c, lane + 64);
+    float dt0 = 0.f, dt1 = 0.f;
+    const int i0 = lane, i1 = lane + 64;
+    for (int jj = 0; jj < nj; ++jj) {
+      const int64_t j = j0 + jj;
+      GPair p;
+      g_pair_forward(a, W1T, B1, W2, c, j, t0, t1, lane, p);
+      const float e = expf(p.a) * (a.hist[j] != tgt ? 1.f : 0.f);
+      const float ds = dsc * e;                                   // dlogit / ds_cj
+      const float da = ds * (p.s - bn);                           // dlogit / da_cj
+      // ReLU + dropout backward: du = da w2 [v > 0] m
+      const float du0 = i0 < a.H ? (p.v0 > 0.f ? da * W2[i0] * p.m0 : 0.f) : 0.f;
+      const float du1 = i1 < a.H ? (p.v1 > 0.f ? da * W2[i1] * p.m1 : 0.f) : 0.f;
+      if (i0 < a.H) {
+        atomicAdd(&GB1[i0], du0);
+        atomicAdd(&GW2[i0], da * fmaxf(p.v0, 0.f));
+      }
+      if (i1 < a.H) {
+        atomicAdd(&GB1[i1], du1);
+        atomicAdd(&GW2[i1], da * fmaxf(p.v1, 0.f));
+      }
+      for (int d = 0; d < a.D; ++d) {                             // dW1[i][d] += du_i x_d
+        const float xd = d < 64 ? rl(p.x0, d) : rl(p.x1, d - 64);
+        if (i0 < a.H) atomicAdd(&GW1[d * HP + i0], du0 * xd);
+        if (i1 < a.H) atomicAdd(&GW1[d * HP + i1], du1 * xd);
+      }
+      if (a.DIN > a.D) {
+        if (i0 < a.H) {
+          atomicAdd(&GW1[a.D * HP + i0], du0 * p.f0);
+          atomicAdd(&GW1[(a.D + 1) * HP + i0], du0 * p.f1);
+        }
+        if (i1 < a.H) {
+          atomicAdd(&GW1[a.D * HP + i1], du1 * p.f0);
+          atomicAdd(&GW1[(a.D + 1) * HP + i1], du1 * p.f1);
+        }
+      }
+      // dx_d = sum_i W1[i][d] du_i for d = lane, lane + 64 (and the two distance features)
+      float dx0 = 0.f, dx1 = 0.f, df0 = 0.f, df1 = 0.f;
+      const int d0 = lane, d1 = lane + 64;
+      for (int i = 0; i < a.H; ++i) {
+        const float dui = i < 64 ? rl(du0, i) : rl(du1, i - 64);
+        if (d0 < a.D) dx0 = fmaf(W1T[d0 * HP + i], dui, dx0);
+        if (d1 < a.D) dx1 = fmaf(W1T[d1 * HP + i], dui, dx1);
+        if (a.DIN > a.D) {
+          df0 = fmaf(W1T[a.D * HP + i], dui, df0);
+          df1 = fmaf(W1T[(a.D + 1) * HP + i], dui, df1);
+        }
+      }
+      const float r0 = dx0 + ds, r1 = dx1 + ds;                   // s = sum(x): ds reaches every dim
+      if (d0 < a.D) atomicAdd(&GH[jj * a.D + d0], r0 * t0);
+      if (d1 < a.D) atomicAdd(&GH[jj * a.D + d1], r1 * t1);
+      dt0 = fmaf(r0, p.h0, dt0);
+      dt1 = fmaf(r1, p.h1, dt1);
+      if (a.DIN > a.D && lane == 0) {                 // sigmoid, then dist_layer (Linear(2, 2))
+        const float q0 = df0 * p.f0 * (1.f - p.f0), q1 = df1 * p.f1 * (1.f - p.f1);
+        atomicAdd(&GDL[0], q0 * p.l0);
+        atomicAdd(&GDL[1], q0 * p.l1);
+        atomicAdd(&GDL[2], q1 * p.l0);
+        atomicAdd(&GDL[3], q1 * p.l1);
+        atomicAdd(&GDL[4], q0);
+        atomicAdd(&GDL[5], q1);
+      }
+    }
+    // target-row gradient (repeated target ids are summed by the atomics)
+    for (int q = 0; q < 2; ++q) {
+      const int d = lane + 64 * q;
+      const float v = q ? dt1 : dt0;
+      if (d >= a.D) continue;
+      if (d < a.IDIM) unsafeAtomicAdd(&g.et[tgt * a.IDIM + d], v);
+      else unsafeAtomicAdd(&g.er[a.treg[c] * a.RDIM + (d - a.IDIM)], v);
+    }
+  }
+  __syncthreads();
+  for (int f = tid; f < a.H * a.DIN; f += GW * 64) {
+    const int i = f / a.DIN, d = f % a.DIN;
+    unsafeAtomicAdd(&g.w1[f], GW1[d * HP + i]);
+  }
+  for (int i = tid; i < a.H; i += GW * 64) {
+    unsafeAtomicAdd(&g.b1[i], GB1[i]);
+    unsafeAtomicAdd(&g.w2[i], GW2[i]);
+  }
+  if (a.DIN > a.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &g.dw[tid] : &g.db[tid - 4], GDL[tid]);
+  for (int f = tid; f < nj * a.D; f += GW * 64) {
+    const int jj = f / a.D, d = f % a.D;
+    const int64_t j = j0 + jj;
+    if (d < a.IDIM) unsafeAtomicAdd(&g.eh[a.hist[j] * a.IDIM + d], GH[f]);
+    else unsafeAtomicAdd(&g.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], GH[f]);
+  }
+}
+
+size_t g_lds_bytes(const GArgs& a, bool backward) {
+  const size_t HP = a.H + 1;
+  size_t f = a.DIN * HP + 2 * a.H;
+  if (backward) f += a.DIN * HP + 2 * a.H + 8 + size_t(a.js) * a.D;
+  return f * sizeof(float);
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 struct TShape {
@@ -931,6 +1213,109 @@ int check_batch(const int64_t* hist, int64_t n, const int64_t* target, int64_t b
 int hip_rc(hipError_t e, const char* what) {
   if (e == hipSuccess) return NAIS_OK;
   return nais_internal_fail(NAIS_E_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+}
+
+// the fused MFMA kernels cover NAIS_basic at D in {8, 16, 32, 64}, H <= 64
+bool fast_ok(const nais_params_t* p) {
+  const int D = p->embed_dim;
+  return p->variant == NAIS_VARIANT_BASIC && (D == 8 || D == 16 || D == 32 || D == 64) &&
+         p->item_dim == D && p->din == D && p->hidden >= 1 && p->hidden <= 64;
+}
+
+int gvalidate(const nais_params_t* p, const nais_train_side_t* side, int64_t b, int64_t n) {
+  if (!p) return nais_internal_fail(NAIS_E_INVALID, "params is NULL");
+  if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
+    return nais_internal_fail(NAIS_E_INVALID, "missing parameter pointer");
+  const int D = p->embed_dim;
+  if (D <= 0 || D > G_MAX_D || p->hidden <= 0 || p->hidden > G_MAX_H)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: embed_dim and hidden must be in [1, 128]");
+  switch (p->variant) {
+    case NAIS_VARIANT_BASIC:
+      if (p->item_dim != D || p->din != D)
+        return nais_internal_fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
+      break;
+    case NAIS_VARIANT_REGION:
+    case NAIS_VARIANT_REGION_DISTANCE: {
+      if (p->item_dim + p->region_dim != D || p->item_dim <= 0 || !p->embed_region)
+        return nais_internal_fail(NAIS_E_INVALID, "region: item_dim + region_dim == embed_dim, embed_region set");
+      const int want = p->variant == NAIS_VARIANT_REGION ? D : D + 2;
+      if (p->din != want) return nais_internal_fail(NAIS_E_INVALID, "region: din must be embed_dim (+2 with distance)");
+      if (p->variant == NAIS_VARIANT_REGION_DISTANCE && (!p->dist_w || !p->dist_b))
+        return nais_internal_fail(NAIS_E_INVALID, "region_distance: dist_w / dist_b missing");
+      if (b > 0 && n > 0 && (!side || !side->hist_region || !side->target_region))
+        return nais_internal_fail(NAIS_E_INVALID, "region variants need side->hist_region / target_region");
+      if (p->variant == NAIS_VARIANT_REGION_DISTANCE && b > 0 && n > 0 &&
+          (!side->target_lat_long || side->latlon_ld < 2 * n))
+        return nais_internal_fail(NAIS_E_INVALID, "region_distance needs side->target_lat_long [b, n, 2]");
+      break;
+    }
+    default:
+      return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: variant must be basic, region or region_distance");
+  }
+  return NAIS_OK;
+}
+
+int g_slice_items(int64_t b, int64_t n) {
+  const int64_t rb = (b + GW - 1) / GW;
+  int64_t js = (n * rb + 511) / 512;   // about 2 workgroups per CU
+  return (int)std::max<int64_t>(1, std::min<int64_t>(G_MAX_JS, js));
+}
+
+GArgs gargs(const nais_params_t* p, const nais_train_side_t* side, const int64_t* hist, int64_t n,
+            const int64_t* target, int64_t b, float dropout_p, uint64_t seed) {
+  GArgs a;
+  a.eh = p->embed_history;
+  a.et = p->embed_target;
+  a.er = p->embed_region;
+  a.w1 = p->w1;
+  a.b1 = p->b1;
+  a.w2 = p->w2;
+  a.dw = p->dist_w;
+  a.db = p->dist_b;
+  a.hist = hist;
+  a.target = target;
+  a.hreg = side ? side->hist_region : nullptr;
+  a.treg = side ? side->target_region : nullptr;
+  a.ll = side ? side->target_lat_long : nullptr;
+  a.ll_ld = side ? side->latlon_ld : 0;
+  a.b = b;
+  a.n = n;
+  a.D = p->embed_dim;
+  a.IDIM = p->variant == NAIS_VARIANT_BASIC ? p->embed_dim : p->item_dim;
+  a.RDIM = p->variant == NAIS_VARIANT_BASIC ? 0 : p->region_dim;
+  a.H = p->hidden;
+  a.DIN = p->din;
+  a.variant = p->variant;
+  a.beta = p->beta;
+  a.dscale = 100.f;   // model.py:265
+  a.js = g_slice_items(b, n);
+  a.drop = make_drop(dropout_p, seed);
+  return a;
+}
+
+size_t g_workspace(int64_t b, int64_t n) {
+  if (b <= 0 || n <= 0) return 0;
+  const int64_t ns = (n + g_slice_items(b, n) - 1) / g_slice_items(b, n);
+  return size_t(2 * ns * b) * sizeof(float);
+}
+
+int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
+  const size_t lds = g_lds_bytes(a, false);
+  static bool once = (set_lds(g_forward_kernel, 160 * 1024), true);
+  (void)once;
+  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + a.js - 1) / a.js));
+  hipLaunchKernelGGL(g_forward_kernel, grid, dim3(GW * 64), lds, st, a, Sp, Np);
+  return nais_internal_check_launch("g_forward_kernel");
+}
+
+int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
+               const GGrads& g, hipStream_t st) {
+  const size_t lds = g_lds_bytes(a, true);
+  static bool once = (set_lds(g_backward_kernel, 160 * 1024), true);
+  (void)once;
+  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + a.js - 1) / a.js));
+  hipLaunchKernelGGL(g_backward_kernel, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g);
+  return nais_internal_check_launch("g_backward_kernel");
 }
 
 }  // namespace
@@ -1055,6 +1440,7 @@ int32_t nais_make_train_batch(const int64_t* indptr, const int64_t* indices, int
 
 size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0 || n <= 0) return 0;
+  if (!fast_ok(params)) return g_workspace(b, n);
   const int js = slice_items(b, n, FWD_PER_CU);
   const int64_t ns = (n + js - 1) / js, rb = (b + TROWS - 1) / TROWS;
   const int64_t D = params->embed_dim, H = params->hidden;
@@ -1063,10 +1449,80 @@ size_t nais_train_workspace_size(const nais_params_t* params, int64_t b, int64_t
   return size_t(std::max(fwd, bwd)) * sizeof(float);
 }
 
+int32_t nais_train_forward_ex(const nais_params_t* params, const nais_train_side_t* side,
+                              const int64_t* hist, int64_t n, const int64_t* target, int64_t b,
+                              float dropout_p, uint64_t seed, float* pred, float* saved,
+                              int32_t* nan_count, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  if (params && fast_ok(params))
+    return nais_train_forward(params, hist, n, target, b, dropout_p, seed, pred, saved, nan_count,
+                              workspace, workspace_bytes, stream);
+  int rc = gvalidate(params, side, b, n);
+  if (rc) return rc;
+  if ((rc = check_batch(hist, n, target, b))) return rc;
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  if (b == 0) return NAIS_OK;
+  if (!pred || !saved) return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n == 0) {
+    hipLaunchKernelGGL(train_finalize_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
+                       nullptr, nullptr, 0, b, n, params->beta, pred, saved, nan_count);
+    return nais_internal_check_launch("train_finalize_kernel");
+  }
+  const GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  const int64_t ns = (n + a.js - 1) / a.js;
+  if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  if (!workspace || workspace_bytes < g_workspace(b, n))
+    return nais_internal_fail(NAIS_E_WORKSPACE, "workspace too small (nais_train_workspace_size)");
+  float* Sp = static_cast<float*>(workspace);
+  float* Np = Sp + ns * b;
+  if ((rc = g_forward(a, Sp, Np, st))) return rc;
+  hipLaunchKernelGGL(train_finalize_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
+                     Sp, Np, (int)ns, b, n, params->beta, pred, saved, nan_count);
+  return nais_internal_check_launch("train_finalize_kernel");
+}
+
+int32_t nais_train_backward_ex(const nais_params_t* params, const nais_train_side_t* side,
+                               const int64_t* hist, int64_t n, const int64_t* target, int64_t b,
+                               float dropout_p, uint64_t seed, const float* pred,
+                               const float* saved, const float* grad_pred,
+                               const nais_train_grads_t* grads, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+  if (!grads) return nais_internal_fail(NAIS_E_INVALID, "grads is NULL");
+  if (params && fast_ok(params))
+    return nais_train_backward(params, hist, n, target, b, dropout_p, seed, pred, saved, grad_pred,
+                               grads->embed_history, grads->embed_target, grads->w1, grads->b1,
+                               grads->w2, workspace, workspace_bytes, stream);
+  int rc = gvalidate(params, side, b, n);
+  if (rc) return rc;
+  if ((rc = check_batch(hist, n, target, b))) return rc;
+  if (!(dropout_p >= 0.f && dropout_p <= 1.f))
+    return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
+  if (b == 0 || n == 0) return NAIS_OK;
+  if (!pred || !saved || !grad_pred || !grads->embed_history || !grads->embed_target || !grads->w1 ||
+      !grads->b1 || !grads->w2)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved/grad pointer");
+  if (params->variant != NAIS_VARIANT_BASIC && !grads->embed_region)
+    return nais_internal_fail(NAIS_E_INVALID, "region variants need grads->embed_region");
+  if (params->variant == NAIS_VARIANT_REGION_DISTANCE && (!grads->dist_w || !grads->dist_b))
+    return nais_internal_fail(NAIS_E_INVALID, "region_distance needs grads->dist_w / dist_b");
+  (void)workspace;
+  (void)workspace_bytes;
+  const GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  if ((n + a.js - 1) / a.js > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
+  const GGrads g{grads->embed_history, grads->embed_target, grads->embed_region, grads->w1,
+                 grads->b1, grads->w2, grads->dist_w, grads->dist_b};
+  return g_backward(a, saved, pred, grad_pred, g, reinterpret_cast<hipStream_t>(stream));
+}
+
 int32_t nais_train_forward(const nais_params_t* params, const int64_t* hist, int64_t n,
                            const int64_t* target, int64_t b, float dropout_p, uint64_t seed,
                            float* pred, float* saved, int32_t* nan_count, void* workspace,
                            size_t workspace_bytes, void* stream) {
+  if (params && !fast_ok(params))
+    return nais_train_forward_ex(params, nullptr, hist, n, target, b, dropout_p, seed, pred, saved,
+                                 nan_count, workspace, workspace_bytes, stream);
   TShape sh;
   int rc = tvalidate(params, &sh);
   if (rc) return rc;
@@ -1102,6 +1558,12 @@ int32_t nais_train_backward(const nais_params_t* params, const int64_t* hist, in
                             float* grad_embed_history, float* grad_embed_target, float* grad_w1,
                             float* grad_b1, float* grad_w2, void* workspace,
                             size_t workspace_bytes, void* stream) {
+  if (params && !fast_ok(params)) {
+    const nais_train_grads_t g{grad_embed_history, grad_embed_target, nullptr, grad_w1, grad_b1,
+                               grad_w2, nullptr, nullptr};
+    return nais_train_backward_ex(params, nullptr, hist, n, target, b, dropout_p, seed, pred, saved,
+                                  grad_pred, &g, workspace, workspace_bytes, stream);
+  }
   TShape sh;
   int rc = tvalidate(params, &sh);
   if (rc) return rc;

@@ -26,7 +26,9 @@ Training (run.py:91-109): `NAIS_basic.forward` in train mode ru
 backward is `nais_train_backward`, so the reference's loop -- forward, `loss_func`, `backward()`,
 optimizer step -- runs unchanged. The batch must be get_NAIS_batch's shape (batches.py:24-50):
 every row shares one history (checked; per-row histories raise). The region variants train on
-the eval-only path for now (train-mode forward raises NotImplementedError).
+the same autograd Function (`nais_train_forward_ex` / `nais_train_backward_ex`, region rows and
+the distance layer included); NAIS_basic at embed_dim <= 64 / hidden <= 64 takes the fused MFMA
+kernels, every other shape (run.py's default factor_num = hidden_dim = 128) a general kernel.
 """
 from __future__ import annotations
 
@@ -127,11 +129,12 @@ class _NAISDevice(nn.Module):
     def _run_forward(self, history, target, history_region=None, target_region=None,
                      target_lat_long=None, sigmoid=True):
         if self.training:
-            if not isinstance(self, NAIS_basic) or not sigmoid:
+            if not sigmoid or self.VARIANT == _capi.VARIANT_DISTANCE:
                 raise NotImplementedError(
                     f"{type(self).__name__}: training-mode {'forward' if sigmoid else 'attention_network'}"
-                    " is implemented for NAIS_basic.forward only (SURVEY.md 8(f1)); call model.eval()")
-            return self._train_forward(history, target)
+                    " is implemented for NAIS_basic / NAIS_regionEmbedding / NAIS_region_distance_Embedding"
+                    ".forward (SURVEY.md 8(f1)); call model.eval()")
+            return self._train_forward(history, target, history_region, target_region, target_lat_long)
         dev = self._check_device(history, target, history_region, target_region, target_lat_long)
         if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
             raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
@@ -183,8 +186,28 @@ class _NAISDevice(nn.Module):
     # False to skip the check (one device->host sync per step) when the caller guarantees it
     check_shared_history = True
 
-    def _train_forward(self, history, target):
-        dev = self._check_device(history, target)
+    def _train_param_names(self):
+        """nais_train_grads_t fields of the parameters the training forward reads."""
+        names = ["embed_history", "embed_target"]
+        if self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE):
+            names.append("embed_region")
+        names += ["w1", "b1", "w2"]
+        if self.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+            names += ["dist_w", "dist_b"]
+        return names
+
+    def _train_params(self):
+        t = {"embed_history": self.embed_history.weight, "embed_target": self.embed_target.weight,
+             "w1": self.attn_layer1.weight, "b1": self.attn_layer1.bias, "w2": self.attn_layer2.weight}
+        if hasattr(self, "embed_region"):
+            t["embed_region"] = self.embed_region.weight
+        if hasattr(self, "dist_layer"):
+            t["dist_w"], t["dist_b"] = self.dist_layer.weight, self.dist_layer.bias
+        return [t[k] for k in self._train_param_names()]
+
+    def _train_forward(self, history, target, history_region=None, target_region=None,
+                       target_lat_long=None):
+        dev = self._check_device(history, target, history_region, target_region, target_lat_long)
         if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
             raise ValueError(f"history must be [b, n] and target [b]; got {tuple(history.shape)}, "
                              f"{tuple(target.shape)}")
@@ -197,14 +220,32 @@ class _NAISDevice(nn.Module):
                 f"{type(self).__name__}: the training step needs rows that share one history "
                 "(get_NAIS_batch, batches.py:24-50); per-row histories are not supported")
         hist = history[0].contiguous() if b > 0 else history.new_empty(0)
-        p = float(self.drop.p) if self.drop.training else 0.0
+        side = None
+        if self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE):
+            if history_region is None or target_region is None:
+                raise ValueError("region variants need history_region and target_region")
+            history_region = history_region.to(torch.int64)
+            if tuple(history_region.shape) != (b, n) or tuple(target_region.shape) != (b,):
+                raise ValueError("history_region must be [b, n] and target_region [b]")
+            if self.check_shared_history and b > 1 and n > 0 and \
+                    not bool((history_region == history_region[:1]).all()):
+                raise NotImplementedError(f"{type(self).__name__}: history_region rows must be shared")
+            ll = None
+            if self.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+                if target_lat_long is None or tuple(target_lat_long.shape) != (b, n, 2):
+                    raise ValueError("target_lat_long must be [b, n, 2]")
+                ll = target_lat_long.to(torch.float32)
+                if not (ll.stride(2) == 1 and ll.stride(1) == 2):
+                    ll = ll.contiguous()
+            hreg = history_region[0].contiguous() if b > 0 else history_region.new_empty(0)
+            side = (hreg, target_region.to(torch.int64).contiguous(), ll)
+        drop = getattr(self, "drop", None)        # none in NAIS_region_distance_Embedding (model.py:268)
+        p = float(drop.p) if drop is not None and drop.training else 0.0
         seed = int(torch.randint(0, 2**62, (1,)).item())   # torch's CPU generator: manual_seed applies
-        w = [self.embed_history.weight, self.embed_target.weight, self.attn_layer1.weight,
-             self.attn_layer1.bias, self.attn_layer2.weight]
-        pred, nan = _NAISTrainStep.apply(self, hist, target, p, seed, *w)
+        pred, nan = _NAISTrainStep.apply(self, hist, target, p, seed, side, *self._train_params())
         self._last_nan = nan
-        if self.report_nan:
-            c = int(nan.item())                              # model.py:50-54
+        if self.report_nan and isinstance(self, NAIS_basic):
+            c = int(nan.item())                              # model.py:50-54 (NAIS_basic only)
             if c > 0:
                 print(c)
         return pred
@@ -219,25 +260,27 @@ class _NAISDevice(nn.Module):
 
 class _NAISTrainStep(torch.autograd.Function):
     """pred = sigmoid(attention_network(...)) of a shared-history batch with dropout; backward
-    through nais_train_backward (gradients of the five NAIS_basic parameters)."""
+    through nais_train_backward_ex (gradients of every parameter the variant's forward reads:
+    the module's `_train_params()`)."""
 
     @staticmethod
-    def forward(ctx, module, hist, target, p, seed, eh, et, w1, b1, w2):
-        dev = eh.device
+    def forward(ctx, module, hist, target, p, seed, side, *weights):
+        dev = weights[0].device
         b, n = target.shape[0], hist.shape[0]
         lib = _capi.load()
         prm = module.nais_params()
+        sd = _train_side(side)
         pred = torch.empty(b, dtype=torch.float32, device=dev)
         saved = torch.empty(2 * max(b, 1), dtype=torch.float32, device=dev)
         nan = torch.zeros(1, dtype=torch.int32, device=dev)
         ws_bytes = lib.nais_train_workspace_size(prm, b, n)
         ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
-        _capi.check(lib.nais_train_forward(prm, _capi.ptr(hist) if n else None, n,
-                                           _capi.ptr(target) if b else None, b, p, seed,
-                                           pred.data_ptr(), saved.data_ptr(), nan.data_ptr(),
-                                           ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
-                    "nais_train_forward")
-        ctx.module, ctx.p, ctx.seed = module, p, seed
+        _capi.check(lib.nais_train_forward_ex(prm, sd, _capi.ptr(hist) if n else None, n,
+                                              _capi.ptr(target) if b else None, b, p, seed,
+                                              pred.data_ptr(), saved.data_ptr(), nan.data_ptr(),
+                                              ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
+                    "nais_train_forward_ex")
+        ctx.module, ctx.p, ctx.seed, ctx.side = module, p, seed, side
         ctx.save_for_backward(hist, target, pred, saved)
         ctx.mark_non_differentiable(nan)
         return pred, nan
@@ -246,25 +289,40 @@ class _NAISTrainStep(torch.autograd.Function):
     def backward(ctx, gpred, _gnan):
         hist, target, pred, saved = ctx.saved_tensors
         m = ctx.module
-        eh, et = m.embed_history.weight, m.embed_target.weight
-        w1, b1, w2 = m.attn_layer1.weight, m.attn_layer1.bias, m.attn_layer2.weight
-        g = [torch.zeros_like(t) for t in (eh, et, w1, b1, w2)]
+        names = m._train_param_names()
+        params = m._train_params()
+        g = [torch.zeros_like(t) for t in params]
+        grads = _capi.NaisTrainGrads()
+        for name, t in zip(names, g):
+            setattr(grads, name, t.data_ptr())
         b, n = target.shape[0], hist.shape[0]
+        dev = params[0].device
         gpred = gpred.to(torch.float32).contiguous()
         lib = _capi.load()
         prm = m.nais_params()
         ws_bytes = lib.nais_train_workspace_size(prm, b, n)
-        ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=eh.device)
-        _capi.check(lib.nais_train_backward(prm, _capi.ptr(hist) if n else None, n,
-                                            _capi.ptr(target) if b else None, b, ctx.p, ctx.seed,
-                                            pred.data_ptr(), saved.data_ptr(), gpred.data_ptr(),
-                                            *[t.data_ptr() for t in g], ws.data_ptr(), ws_bytes,
-                                            _capi.stream_handle(eh.device)),
-                    "nais_train_backward")
+        ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
+        _capi.check(lib.nais_train_backward_ex(prm, _train_side(ctx.side), _capi.ptr(hist) if n else None,
+                                               n, _capi.ptr(target) if b else None, b, ctx.p, ctx.seed,
+                                               pred.data_ptr(), saved.data_ptr(), gpred.data_ptr(),
+                                               grads, ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
+                    "nais_train_backward_ex")
         # rows of the embedding tables this step can have touched (for optim.Adagrad's row update)
-        _note_rows(eh, hist)
-        _note_rows(et, target)
-        return (None, None, None, None, None, *g)
+        _note_rows(m.embed_history.weight, hist)
+        _note_rows(m.embed_target.weight, target)
+        if "embed_region" in names:
+            _note_rows(m.embed_region.weight, torch.cat([ctx.side[0], ctx.side[1]]))
+        return (None, None, None, None, None, None, *g)
+
+
+def _train_side(side):
+    sd = _capi.NaisTrainSide()
+    if side is not None:
+        hreg, treg, ll = side
+        sd.hist_region, sd.target_region = _capi.ptr(hreg), _capi.ptr(treg)
+        if ll is not None:
+            sd.target_lat_long, sd.latlon_ld = ll.data_ptr(), ll.stride(0)
+    return sd
 
 
 def _note_rows(param, rows):

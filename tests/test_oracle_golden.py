@@ -253,3 +253,26 @@ def test_forward_disentangled(tag, n):
     c = z["coords"]
     mine = np.array([[powerlaw_oracle.dist(c[a], c[h]) for h in hist] for a in tgt], dtype=np.float32)
     assert np.array_equal(mine, dist)
+
+
+@pytest.mark.parametrize("case", ["region", "region_distance", "basic128"])
+def test_train_oracle_region_variants_match_reference(case):
+    """The training restatement for NAIS_regionEmbedding / NAIS_region_distance_Embedding and
+    NAIS_basic at run.py's default D = H = 128 vs the reference's autograd
+    (tests/golden/make_golden_train_region.py)."""
+    from oracle import train_oracle
+    z = load_golden("train_step_region.npz")
+    pre = case + "/"
+    p = {k[len(pre) + 2:]: z[k] for k in z.files if k.startswith(pre + "p/")}
+    kw = {}
+    if case != "basic128":
+        kw.update(hist_region=z[pre + "hist_region"], data_region=z[pre + "data_region"])
+    if case == "region_distance":
+        kw["latlon"] = z[pre + "latlon"]
+    r = train_oracle.train_step(p, z[pre + "hist"], z[pre + "data"], z[pre + "labels"], **kw)
+    assert np.max(np.abs(r["pred"] - z[pre + "pred"])) <= 1e-6
+    assert abs(r["loss"] - float(z[pre + "loss"])) <= 1e-6
+    assert set(r["grads"]) == {k[len(pre) + 5:] for k in z.files if k.startswith(pre + "grad/")}
+    for k, g in r["grads"].items():
+        ref = z[pre + "grad/" + k]
+        assert np.max(np.abs(g.reshape(ref.shape) - ref)) <= 2e-6 * np.abs(ref).max(), k
