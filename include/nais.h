@@ -438,7 +438,8 @@ int32_t nais_train_backward_ex(const nais_params_t* params, const nais_train_sid
                                size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Fused training step (run.py:101-109 in one call): forward, BCELoss (model.py:21) added into
+ * Fused training step of NAIS_basic (run.py:101-109 in one call; embed_dim / hidden up to 128,
+ * the fused MFMA kernels where they apply, else the general ones): forward, BCELoss (model.py:21) added into
  * *loss_sum (device float, mean over the b rows -- run.py's train_loss accumulates loss.item()),
  * backward, and torch.optim.Adagrad's update of all five parameters IN PLACE (the params pointers
  * are written). Adagrad state lives in nais_adagrad_state_t; its gradient scratch must be all zero

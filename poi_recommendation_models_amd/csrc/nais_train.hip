@@ -659,7 +659,7 @@ __global__ void adagrad_rows_kernel(float* __restrict__ p, float* __restrict__ s
 // leaves zero again): the small tensors element-wise; the embedding tables row by row for the rows
 // the batch touched (history + targets; with weight_decay 0 the other rows' dense update is the
 // identity). A row listed twice is claimed once per step through `stamp` (atomicExch of the step
-// number), so it is updated once, with its summed gradient. One wave per row, lane = dim (D <= 64).
+// number), so it is updated once, with its summed gradient. One wave per row, lanes over dims.
 struct StepOpt {
   float* p_eh;
   float* p_et;
@@ -709,8 +709,8 @@ __global__ void step_adagrad_kernel(StepOpt o, int H, int D, const int64_t* __re
     if (item >= 2 * dense_rows) return;
     const bool tgt = item >= dense_rows;
     const int64_t row = tgt ? item - dense_rows : item;
-    if (lane < D) {
-      const int64_t i = row * D + lane;
+    for (int d = lane; d < D; d += 64) {
+      const int64_t i = row * D + d;
       if (tgt) adagrad_elem(o.p_et + i, o.s_et + i, o.g_et + i, o.clr, o.wd, o.eps);
       else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, o.wd, o.eps);
     }
@@ -722,10 +722,12 @@ __global__ void step_adagrad_kernel(StepOpt o, int H, int D, const int64_t* __re
   int claimed = 0;
   if (lane == 0) claimed = atomicExch(tgt ? o.st_et + row : o.st_eh + row, o.tag) != o.tag;
   claimed = __shfl(claimed, 0);
-  if (claimed && lane < D) {
-    const int64_t i = row * D + lane;
-    if (tgt) adagrad_elem(o.p_et + i, o.s_et + i, o.g_et + i, o.clr, 0.f, o.eps);
-    else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, 0.f, o.eps);
+  if (claimed) {
+    for (int d = lane; d < D; d += 64) {
+      const int64_t i = row * D + d;
+      if (tgt) adagrad_elem(o.p_et + i, o.s_et + i, o.g_et + i, o.clr, 0.f, o.eps);
+      else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, 0.f, o.eps);
+    }
   }
 }
 
@@ -841,7 +843,6 @@ make_batch_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict_
 // registers.
 // ---------------------------------------------------------------------------------------------
 constexpr int GW = 8;                 // rows (waves) per workgroup
-constexpr int G_MAX_JS = 32;          // items per slice
 constexpr int G_MAX_D = 128, G_MAX_H = 128, G_MAX_DIN = G_MAX_D + 2;
 
 struct GArgs {
@@ -876,235 +877,358 @@ __device__ __forceinline__ float tfull(const GArgs& a, int64_t c, int d) {
   return a.er[a.treg[c] * a.RDIM + (d - a.IDIM)];
 }
 
-struct GPair {
-  float h0, h1, x0, x1;   // hf and x at dims lane, lane + 64
-  float f0, f1;           // distance features x[D], x[D+1] (region_distance), wave-uniform
-  float l0, l1;           // 100 * latlon (region_distance)
-  float v0, v1;           // post-dropout hidden units lane, lane + 64
-  float m0, m1;           // dropout factors
-  float s, a;             // h . t and the attention logit
+// LDS image of the general kernels (floats). Hidden rows are padded to HB*32 (zeros), x to
+// DINP = DIN rounded up to even (K-steps of 2); pitches are odd so that every MFMA operand read
+// (lanes over rows at a fixed column, or over columns at a fixed row) is bank-conflict-free.
+struct GL {
+  int HB, HP32, DINP, Q;        // hidden blocks, padded hidden, padded din, W1 pitch (DINP + 1)
+  int HD;                       // history-slice row pitch (D + 1)
+  int DBX, XP, UP;              // x blocks of the dW1 tiles (ceil(DIN/32)), stage pitches
+  int o_w1, o_b1, o_w2, o_hs, o_ts, o_fs, fwd;
+  int o_gh, o_su, o_sx, o_gb, o_gw, o_gd, bwd;
+  __host__ __device__ GL(int D, int H, int DIN) {
+    HB = (H + 31) / 32;
+    HP32 = HB * 32;
+    DINP = (DIN + 1) & ~1;
+    Q = DINP + 1;
+    HD = D + 1;
+    DBX = (DIN + 31) / 32;
+    XP = DBX * 32 + 1;
+    UP = HP32 + 1;
+    o_w1 = 0;
+    o_b1 = o_w1 + HP32 * Q;
+    o_w2 = o_b1 + HP32;
+    o_hs = o_w2 + HP32;                 // [32][HD] full history rows of the slice
+    o_ts = o_hs + 32 * HD;              // [GW][D]  full target rows of the workgroup
+    o_fs = o_ts + GW * D;               // [GW][32][4] f0, f1, 100 lat, 100 lng (region_distance)
+    fwd = o_fs + GW * 32 * 4;
+    o_gh = fwd;                         // [32][D]  history-row grads of the slice
+    o_su = o_gh + 32 * D;               // [32][UP] du^T stage (one wave's pairs)
+    o_sx = o_su + 32 * UP;              // [32][XP] x stage
+    o_gb = o_sx + 32 * XP;              // [HP32] db1
+    o_gw = o_gb + HP32;                 // [HP32] dw2
+    o_gd = o_gw + HP32;                 // [8]    dist_layer dw | db
+    bwd = o_gd + 8;
+  }
 };
 
-__device__ __forceinline__ void g_pair_forward(const GArgs& a, const float* W1T, const float* B1,
-                                               const float* W2, int64_t c, int64_t j, float t0,
-                                               float t1, int lane, GPair& p) {
-  const int HP = a.H + 1;
-  p.h0 = hfull(a, j, lane);
-  p.h1 = hfull(a, j, lane + 64);
-  p.x0 = p.h0 * t0;
-  p.x1 = p.h1 * t1;
-  float sp = p.x0 + p.x1;
-  for (int o = 32; o > 0; o >>= 1) sp += __shfl_xor(sp, o);
-  p.s = sp;
-  p.f0 = p.f1 = p.l0 = p.l1 = 0.f;
-  if (a.variant == NAIS_VARIANT_REGION_DISTANCE) {
-    const float* ll = a.ll + c * a.ll_ld + 2 * j;
-    p.l0 = ll[0] * a.dscale;
-    p.l1 = ll[1] * a.dscale;
-    // sigmoid(dist_layer(100 ll)), model.py:265, in the scorer's operation order
-    p.f0 = 1.0f / (1.0f + expf(-(p.l0 * a.dw[0] + p.l1 * a.dw[1] + a.db[0])));
-    p.f1 = 1.0f / (1.0f + expf(-(p.l0 * a.dw[2] + p.l1 * a.dw[3] + a.db[1])));
+// stage W1 (row-major, pitch Q, zero padded), b1, w2, the slice's full history rows and the
+// workgroup's full target rows (+ the distance features of every (row, item) pair)
+__device__ void gm_stage(const GArgs& a, const GL& g, float* L, int tid, int64_t c0, int64_t j0,
+                         int nj) {
+  constexpr int NT = GW * 64;
+  for (int f = tid; f < g.HP32 * g.Q; f += NT) {
+    const int i = f / g.Q, k = f % g.Q;
+    L[g.o_w1 + f] = (i < a.H && k < a.DIN) ? a.w1[int64_t(i) * a.DIN + k] : 0.f;
   }
-  const int i0 = lane, i1 = lane + 64;
-  float u0 = i0 < a.H ? B1[i0] : 0.f, u1 = i1 < a.H ? B1[i1] : 0.f;
-  const int dmain = a.D;
-  for (int d = 0; d < dmain; ++d) {
-    const float xd = d < 64 ? rl(p.x0, d) : rl(p.x1, d - 64);
-    u0 = fmaf(W1T[d * HP + i0], xd, u0);
-    if (a.H > 64) u1 = fmaf(W1T[d * HP + i1], xd, u1);
+  for (int i = tid; i < g.HP32; i += NT) {
+    L[g.o_b1 + i] = i < a.H ? a.b1[i] : 0.f;
+    L[g.o_w2 + i] = i < a.H ? a.w2[i] : 0.f;
+  }
+  for (int f = tid; f < 32 * g.HD; f += NT) {
+    const int n = f / g.HD, d = f % g.HD;
+    L[g.o_hs + f] = (n < nj && d < a.D) ? hfull(a, j0 + n, d) : 0.f;
+  }
+  for (int f = tid; f < GW * a.D; f += NT) {
+    const int w = f / a.D, d = f % a.D;
+    const int64_t c = c0 + w;
+    L[g.o_ts + f] = c < a.b ? tfull(a, c, d) : 0.f;
   }
   if (a.DIN > a.D) {
-    u0 = fmaf(W1T[a.D * HP + i0], p.f0, u0);
-    u0 = fmaf(W1T[(a.D + 1) * HP + i0], p.f1, u0);
-    if (a.H > 64) {
-      u1 = fmaf(W1T[a.D * HP + i1], p.f0, u1);
-      u1 = fmaf(W1T[(a.D + 1) * HP + i1], p.f1, u1);
+    for (int f = tid; f < GW * 32; f += NT) {
+      const int w = f / 32, n = f % 32;
+      const int64_t c = c0 + w;
+      float f0 = 0.f, f1 = 0.f, l0 = 0.f, l1 = 0.f;
+      if (c < a.b && n < nj) {
+        const float* ll = a.ll + c * a.ll_ld + 2 * (j0 + n);
+        l0 = ll[0] * a.dscale;
+        l1 = ll[1] * a.dscale;
+        // sigmoid(dist_layer(100 ll)), model.py:265, in the scorer's operation order
+        f0 = 1.0f / (1.0f + expf(-(l0 * a.dw[0] + l1 * a.dw[1] + a.db[0])));
+        f1 = 1.0f / (1.0f + expf(-(l0 * a.dw[2] + l1 * a.dw[3] + a.db[1])));
+      }
+      float* o = L + g.o_fs + f * 4;
+      o[0] = f0;
+      o[1] = f1;
+      o[2] = l0;
+      o[3] = l1;
     }
   }
-  p.m0 = p.m1 = 1.f;
-  if (a.drop.on) {
-    const uint32_t k = a.drop.key(uint32_t(c * a.n + j));
-    p.m0 = a.drop.factor(k, i0);
-    p.m1 = a.drop.factor(k, i1);
-  }
-  p.v0 = i0 < a.H ? u0 * p.m0 : 0.f;
-  p.v1 = i1 < a.H ? u1 * p.m1 : 0.f;
-  float ap = (i0 < a.H ? W2[i0] * fmaxf(p.v0, 0.f) : 0.f);
-  if (i1 < a.H) ap = fmaf(W2[i1], fmaxf(p.v1, 0.f), ap);
-  for (int o = 32; o > 0; o >>= 1) ap += __shfl_xor(ap, o);
-  p.a = ap;
 }
 
-// LDS: W1T [DIN][H+1] | b1 [H] | w2 [H]   (+ backward: dW1 [DIN][H+1] | db1 [H] | dw2 [H] |
-//      d(dist_layer) [8] | dhist [js][D])
-__device__ void g_stage(const GArgs& a, float* L, int tid, int nthreads) {
-  const int HP = a.H + 1;
-  for (int f = tid; f < a.H * a.DIN; f += nthreads) {
-    const int i = f / a.DIN, d = f % a.DIN;
-    L[d * HP + i] = a.w1[f];
-  }
-  float* B1 = L + a.DIN * HP;
-  for (int i = tid; i < a.H; i += nthreads) {
-    B1[i] = a.b1[i];
-    B1[a.H + i] = a.w2[i];
-  }
+// x[k][n] of the wave's row and item n (0 past din)
+__device__ __forceinline__ float gm_x(const GArgs& a, const GL& g, const float* L, int w, int n,
+                                      int k) {
+  if (k < a.D) return L[g.o_hs + n * g.HD + k] * L[g.o_ts + w * a.D + k];
+  if (k < a.DIN) return L[g.o_fs + (w * 32 + n) * 4 + (k - a.D)];
+  return 0.f;
 }
 
+// Forward of the wave's 32 pairs (row c, items j0 + n): acc[hb] = dropout(b1 + W1 x) in the
+// 32x32 C layout (rows = hidden units, columns = pairs), the pair's h . t and attention logit.
+template <int HBM>
+__device__ __forceinline__ void gm_pair_forward(const GArgs& a, const GL& g, const float* L, int w,
+                                                int lane, int64_t c, int64_t j0, floatx16 (&acc)[HBM],
+                                                float& sdot, float& alogit) {
+  const int hh = lane >> 5, n = lane & 31;
+#pragma unroll
+  for (int hb = 0; hb < HBM; ++hb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[hb][r] = hb < g.HB ? L[g.o_b1 + crow(hb, r, hh)] : 0.f;
+  float sp = 0.f;
+  for (int t = 0; t < g.DINP / 2; ++t) {
+    const int k = 2 * t + hh;
+    const float x = gm_x(a, g, L, w, n, k);
+    if (k < a.D) sp += x;
+#pragma unroll
+    for (int hb = 0; hb < HBM; ++hb)
+      if (hb < g.HB) acc[hb] = mfma(L[g.o_w1 + (32 * hb + n) * g.Q + k], x, acc[hb]);
+  }
+  sdot = sp + __shfl_xor(sp, 32);
+  float ap = 0.f;
+  const uint32_t key = a.drop.on ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
+#pragma unroll
+  for (int hb = 0; hb < HBM; ++hb) {
+    if (hb >= g.HB) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = crow(hb, r, hh);
+      float v = acc[hb][r];
+      if (a.drop.on) v *= a.drop.factor(key, i);
+      acc[hb][r] = v;
+      ap = fmaf(L[g.o_w2 + i], fmaxf(v, 0.f), ap);
+    }
+  }
+  alogit = ap + __shfl_xor(ap, 32);
+}
+
+// sum over the 32 lanes of one half (both halves get it)
+__device__ __forceinline__ float half_sum(float v) {
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int HBM>
 __global__ void __launch_bounds__(GW * 64)
-g_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
+gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
   extern __shared__ float4 glds4[];
   float* L = reinterpret_cast<float*>(glds4);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int64_t c = int64_t(blockIdx.x) * GW + (tid >> 6);
-  const int64_t j0 = int64_t(blockIdx.y) * a.js;
-  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
-  g_stage(a, L, tid, GW * 64);
+  const GL g(a.D, a.H, a.DIN);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
+  const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
+  const int64_t j0 = int64_t(blockIdx.y) * 32;
+  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+  gm_stage(a, g, L, tid, c0, j0, nj);
   __syncthreads();
   if (c >= a.b) return;   // no barriers below
-  const int HP = a.H + 1;
-  const float* W1T = L;
-  const float* B1 = L + a.DIN * HP;
-  const float* W2 = B1 + a.H;
-  const float t0 = tfull(a, c, lane), t1 = tfull(a, c, lane + 64);
-  const int64_t tgt = a.target[c];
-  float S = 0.f, N = 0.f;
-  for (int jj = 0; jj < nj; ++jj) {
-    const int64_t j = j0 + jj;
-    GPair p;
-    g_pair_forward(a, W1T, B1, W2, c, j, t0, t1, lane, p);
-    const float e = expf(p.a) * (a.hist[j] != tgt ? 1.f : 0.f);   // model.py:74-78
-    S += e;
-    N = fmaf(e, p.s, N);
-  }
+  floatx16 acc[HBM];
+  float sdot, at;
+  gm_pair_forward<HBM>(a, g, L, w, lane, c, j0, acc, sdot, at);
+  float e = 0.f;
+  if (n < nj) e = expf(at) * (a.hist[j0 + n] != a.target[c] ? 1.f : 0.f);   // model.py:74-78
+  const float S = half_sum(e), N = half_sum(e * sdot);
   if (lane == 0) {
     Sp[int64_t(blockIdx.y) * a.b + c] = S;
     Np[int64_t(blockIdx.y) * a.b + c] = N;
   }
 }
 
-__global__ void __launch_bounds__(GW * 64)
-g_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
-                  const float* __restrict__ gpred, GGrads g) {
+template <int HBM>
+__global__ void __launch_bounds__(GW * 64, 1)
+gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
+                   const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows) {
+  if (bad_rows && *bad_rows) return;   // fused step on a NaN batch: no update (see train_loss)
   extern __shared__ float4 glds4[];
   float* L = reinterpret_cast<float*>(glds4);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int HP = a.H + 1;
-  const int64_t c = int64_t(blockIdx.x) * GW + (tid >> 6);
-  const int64_t j0 = int64_t(blockIdx.y) * a.js;
-  const int nj = (int)(a.n - j0 < a.js ? a.n - j0 : a.js);
-  float* W1T = L;
-  float* B1 = L + a.DIN * HP;
-  float* W2 = B1 + a.H;
-  float* GW1 = W2 + a.H;                 // [DIN][HP]
-  float* GB1 = GW1 + a.DIN * HP;         // [H]
-  float* GW2 = GB1 + a.H;                // [H]
-  float* GDL = GW2 + a.H;                // dist_layer: dw [4] | db [2]   (8 reserved)
-  float* GH = GDL + 8;                   // [js][D]
-  g_stage(a, L, tid, GW * 64);
-  const int acc_n = a.DIN * HP + 2 * a.H + 8 + nj * a.D;
-  for (int f = tid; f < acc_n; f += GW * 64) GW1[f] = 0.f;
+  const GL g(a.D, a.H, a.DIN);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31, hh = lane >> 5;
+  const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
+  const bool live = c < a.b;
+  const int64_t j0 = int64_t(blockIdx.y) * 32;
+  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+  gm_stage(a, g, L, tid, c0, j0, nj);
+  for (int f = tid; f < 32 * a.D; f += GW * 64) L[g.o_gh + f] = 0.f;
+  for (int f = tid; f < 2 * g.HP32 + 8; f += GW * 64) L[g.o_gb + f] = 0.f;
   __syncthreads();
-  if (c < a.b) {
-    const int64_t tgt = a.target[c];
+
+  // ---- recompute the forward, then du in place (C layout)
+  floatx16 acc[HBM];
+  float sdot = 0.f, at = 0.f;
+  const int64_t tgt = live ? a.target[c] : -1;
+  float e = 0.f;
+  if (live) {
+    gm_pair_forward<HBM>(a, g, L, w, lane, c, j0, acc, sdot, at);
+    if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
+  } else {
+#pragma unroll
+    for (int hb = 0; hb < HBM; ++hb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[hb][r] = 0.f;
+  }
+  float ds = 0.f, da = 0.f;
+  if (live) {
     const float S = saved[c], N = saved[a.b + c], pc = pred[c];
-    const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid, model.py:55)
+    const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid)
     const float Sb = (a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta);
-    const float dsc = gl / Sb, bn = a.beta * N / S;
-    const float t0 = tfull(a, c, lane), t1 = tfull(a, c, lane + 64);
-    float dt0 = 0.f, dt1 = 0.f;
-    const int i0 = lane, i1 = lane + 64;
-    for (int jj = 0; jj < nj; ++jj) {
-      const int64_t j = j0 + jj;
-      GPair p;
-      g_pair_forward(a, W1T, B1, W2, c, j, t0, t1, lane, p);
-      const float e = expf(p.a) * (a.hist[j] != tgt ? 1.f : 0.f);
-      const float ds = dsc * e;                                   // dlogit / ds_cj
-      const float da = ds * (p.s - bn);                           // dlogit / da_cj
-      // ReLU + dropout backward: du = da w2 [v > 0] m
-      const float du0 = i0 < a.H ? (p.v0 > 0.f ? da * W2[i0] * p.m0 : 0.f) : 0.f;
-      const float du1 = i1 < a.H ? (p.v1 > 0.f ? da * W2[i1] * p.m1 : 0.f) : 0.f;
-      if (i0 < a.H) {
-        atomicAdd(&GB1[i0], du0);
-        atomicAdd(&GW2[i0], da * fmaxf(p.v0, 0.f));
-      }
-      if (i1 < a.H) {
-        atomicAdd(&GB1[i1], du1);
-        atomicAdd(&GW2[i1], da * fmaxf(p.v1, 0.f));
-      }
-      for (int d = 0; d < a.D; ++d) {                             // dW1[i][d] += du_i x_d
-        const float xd = d < 64 ? rl(p.x0, d) : rl(p.x1, d - 64);
-        if (i0 < a.H) atomicAdd(&GW1[d * HP + i0], du0 * xd);
-        if (i1 < a.H) atomicAdd(&GW1[d * HP + i1], du1 * xd);
-      }
-      if (a.DIN > a.D) {
-        if (i0 < a.H) {
-          atomicAdd(&GW1[a.D * HP + i0], du0 * p.f0);
-          atomicAdd(&GW1[(a.D + 1) * HP + i0], du0 * p.f1);
-        }
-        if (i1 < a.H) {
-          atomicAdd(&GW1[a.D * HP + i1], du1 * p.f0);
-          atomicAdd(&GW1[(a.D + 1) * HP + i1], du1 * p.f1);
-        }
-      }
-      // dx_d = sum_i W1[i][d] du_i for d = lane, lane + 64 (and the two distance features)
-      float dx0 = 0.f, dx1 = 0.f, df0 = 0.f, df1 = 0.f;
-      const int d0 = lane, d1 = lane + 64;
-      for (int i = 0; i < a.H; ++i) {
-        const float dui = i < 64 ? rl(du0, i) : rl(du1, i - 64);
-        if (d0 < a.D) dx0 = fmaf(W1T[d0 * HP + i], dui, dx0);
-        if (d1 < a.D) dx1 = fmaf(W1T[d1 * HP + i], dui, dx1);
-        if (a.DIN > a.D) {
-          df0 = fmaf(W1T[a.D * HP + i], dui, df0);
-          df1 = fmaf(W1T[(a.D + 1) * HP + i], dui, df1);
-        }
-      }
-      const float r0 = dx0 + ds, r1 = dx1 + ds;                   // s = sum(x): ds reaches every dim
-      if (d0 < a.D) atomicAdd(&GH[jj * a.D + d0], r0 * t0);
-      if (d1 < a.D) atomicAdd(&GH[jj * a.D + d1], r1 * t1);
-      dt0 = fmaf(r0, p.h0, dt0);
-      dt1 = fmaf(r1, p.h1, dt1);
-      if (a.DIN > a.D && lane == 0) {                 // sigmoid, then dist_layer (Linear(2, 2))
-        const float q0 = df0 * p.f0 * (1.f - p.f0), q1 = df1 * p.f1 * (1.f - p.f1);
-        atomicAdd(&GDL[0], q0 * p.l0);
-        atomicAdd(&GDL[1], q0 * p.l1);
-        atomicAdd(&GDL[2], q1 * p.l0);
-        atomicAdd(&GDL[3], q1 * p.l1);
-        atomicAdd(&GDL[4], q0);
-        atomicAdd(&GDL[5], q1);
-      }
+    ds = gl / Sb * e;                                           // dlogit / ds_cj
+    da = ds * (sdot - a.beta * N / S);                          // dlogit / da_cj
+  }
+  const uint32_t key = (live && a.drop.on) ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
+  // du in place; db1 / dw2 as sums over the 32 pairs of each half (reduce-scatter), LDS atomics
+#pragma unroll
+  for (int hb = 0; hb < HBM; ++hb) {
+    if (hb >= g.HB) continue;
+    float vb[16], vz[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = crow(hb, r, hh);
+      const float v = acc[hb][r];
+      const float m = a.drop.on ? a.drop.factor(key, i) : 1.f;
+      const float du = v > 0.f ? da * L[g.o_w2 + i] * m : 0.f;   // ReLU + dropout backward
+      acc[hb][r] = du;
+      vb[r] = du;
+      vz[r] = da * fmaxf(v, 0.f);
     }
-    // target-row gradient (repeated target ids are summed by the atomics)
-    for (int q = 0; q < 2; ++q) {
-      const int d = lane + 64 * q;
-      const float v = q ? dt1 : dt0;
-      if (d >= a.D) continue;
-      if (d < a.IDIM) unsafeAtomicAdd(&g.et[tgt * a.IDIM + d], v);
-      else unsafeAtomicAdd(&g.er[a.treg[c] * a.RDIM + (d - a.IDIM)], v);
+    const float tb = half_reduce_scatter<16>(vb, lane);
+    const float tz = half_reduce_scatter<16>(vz, lane);
+    if ((n & 1) == 0 && live) {
+      const int i = crow(hb, n >> 1, hh);
+      atomicAdd(&L[g.o_gb + i], tb);
+      atomicAdd(&L[g.o_gw + i], tz);
     }
   }
-  __syncthreads();
-  for (int f = tid; f < a.H * a.DIN; f += GW * 64) {
-    const int i = f / a.DIN, d = f % a.DIN;
-    unsafeAtomicAdd(&g.w1[f], GW1[d * HP + i]);
+  // ---- dx = W1^T du (K-step (hb, r) = hidden unit crow(hb, r, hh): du straight from acc)
+  constexpr int DBM = 4;
+  floatx16 dx[DBM];
+  const int DB = (a.D + 31) / 32;
+#pragma unroll
+  for (int q = 0; q < DBM; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dx[q][r] = 0.f;
+  float df0 = 0.f, df1 = 0.f;
+#pragma unroll
+  for (int hb = 0; hb < HBM; ++hb) {
+    if (hb >= g.HB) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = crow(hb, r, hh);
+      const float du = acc[hb][r];
+      const float* wrow = L + g.o_w1 + i * g.Q;
+#pragma unroll
+      for (int q = 0; q < DBM; ++q)
+        if (q < DB) dx[q] = mfma(wrow[32 * q + n], du, dx[q]);
+      if (a.DIN > a.D) {
+        df0 = fmaf(wrow[a.D], du, df0);
+        df1 = fmaf(wrow[a.D + 1], du, df1);
+      }
+    }
+  }
+  // ---- r = dx + ds: history-row grads (LDS atomics per item) and the target-row grad
+#pragma unroll
+  for (int q = 0; q < DBM; ++q) {
+    if (q >= DB) continue;
+    float vt[16];
+    // the lane holds dx[d][pair n] for the C-tile rows d = 32 q + crow(0, r, hh)
+    // (LDS atomics for the history-row grads: keeping r live until a per-wave round instead
+    // costs registers and measured slower, 0.84 vs 0.77 ms at D = H = 128)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = 32 * q + crow(0, r, hh);
+      vt[r] = 0.f;
+      if (d < a.D && live && n < nj) {
+        const float rv = dx[q][r] + ds;
+        atomicAdd(&L[g.o_gh + n * a.D + d], rv * L[g.o_ts + w * a.D + d]);
+        vt[r] = rv * L[g.o_hs + n * g.HD + d];
+      }
+    }
+    const float tt = half_reduce_scatter<16>(vt, lane);
+    const int d = 32 * q + crow(0, n >> 1, hh);
+    if ((n & 1) == 0 && live && d < a.D) {
+      if (d < a.IDIM) unsafeAtomicAdd(&gr.et[tgt * a.IDIM + d], tt);
+      else unsafeAtomicAdd(&gr.er[a.treg[c] * a.RDIM + (d - a.IDIM)], tt);
+    }
+  }
+  if (a.DIN > a.D) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the wave's pairs
+    df0 += __shfl_xor(df0, 32);
+    df1 += __shfl_xor(df1, 32);
+    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live && n < nj && hh == 0) {
+      const float* fs = L + g.o_fs + (w * 32 + n) * 4;
+      const float q0 = df0 * fs[0] * (1.f - fs[0]), q1 = df1 * fs[1] * (1.f - fs[1]);
+      qv[0] = q0 * fs[2];
+      qv[1] = q0 * fs[3];
+      qv[2] = q1 * fs[2];
+      qv[3] = q1 * fs[3];
+      qv[4] = q0;
+      qv[5] = q1;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const float t = half_sum(qv[k]);
+      if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
+    }
+  }
+  // ---- dW1 = sum over the workgroup's pairs of du x^T: each wave's 32 pairs staged in turn,
+  // every wave accumulating the output tiles it owns (tiles w, w + GW, w + 2 GW)
+  constexpr int OWN = 3;
+  floatx16 gw[OWN];
+#pragma unroll
+  for (int q = 0; q < OWN; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gw[q][r] = 0.f;
+  const int ntile = g.HB * g.DBX;
+  for (int rd = 0; rd < GW; ++rd) {
+    if (w == rd) {
+#pragma unroll
+      for (int hb = 0; hb < HBM; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (hb < g.HB) L[g.o_su + n * g.UP + crow(hb, r, hh)] = acc[hb][r];
+      for (int d = hh; d < g.DBX * 32; d += 2)
+        L[g.o_sx + n * g.XP + d] = (live && n < nj) ? gm_x(a, g, L, w, n, d) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < OWN; ++q) {
+      const int tile = w + q * GW;
+      if (tile >= ntile) continue;
+      const int ib = tile / g.DBX, xb = tile % g.DBX;
+#pragma unroll 4
+      for (int t = 0; t < 16; ++t) {
+        const int p = 2 * t + hh;
+        gw[q] = mfma(L[g.o_su + p * g.UP + 32 * ib + n], L[g.o_sx + p * g.XP + 32 * xb + n], gw[q]);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- flush: dW1 tiles, db1 / dw2, dist_layer, the slice's history-row grads
+#pragma unroll
+  for (int q = 0; q < OWN; ++q) {
+    const int tile = w + q * GW;
+    if (tile >= ntile) continue;
+    const int ib = tile / g.DBX, xb = tile % g.DBX;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * ib + crow(0, r, hh), d = 32 * xb + n;
+      if (i < a.H && d < a.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * a.DIN + d], gw[q][r]);
+    }
   }
   for (int i = tid; i < a.H; i += GW * 64) {
-    unsafeAtomicAdd(&g.b1[i], GB1[i]);
-    unsafeAtomicAdd(&g.w2[i], GW2[i]);
+    unsafeAtomicAdd(&gr.b1[i], L[g.o_gb + i]);
+    unsafeAtomicAdd(&gr.w2[i], L[g.o_gw + i]);
   }
-  if (a.DIN > a.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &g.dw[tid] : &g.db[tid - 4], GDL[tid]);
+  if (a.DIN > a.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], L[g.o_gd + tid]);
   for (int f = tid; f < nj * a.D; f += GW * 64) {
     const int jj = f / a.D, d = f % a.D;
     const int64_t j = j0 + jj;
-    if (d < a.IDIM) unsafeAtomicAdd(&g.eh[a.hist[j] * a.IDIM + d], GH[f]);
-    else unsafeAtomicAdd(&g.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], GH[f]);
+    if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], L[g.o_gh + f]);
+    else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], L[g.o_gh + f]);
   }
 }
 
 size_t g_lds_bytes(const GArgs& a, bool backward) {
-  const size_t HP = a.H + 1;
-  size_t f = a.DIN * HP + 2 * a.H;
-  if (backward) f += a.DIN * HP + 2 * a.H + 8 + size_t(a.js) * a.D;
-  return f * sizeof(float);
+  const GL g(a.D, a.H, a.DIN);
+  return size_t(backward ? g.bwd : g.fwd) * sizeof(float);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1255,11 +1379,7 @@ int gvalidate(const nais_params_t* p, const nais_train_side_t* side, int64_t b, 
   return NAIS_OK;
 }
 
-int g_slice_items(int64_t b, int64_t n) {
-  const int64_t rb = (b + GW - 1) / GW;
-  int64_t js = (n * rb + 511) / 512;   // about 2 workgroups per CU
-  return (int)std::max<int64_t>(1, std::min<int64_t>(G_MAX_JS, js));
-}
+int g_slice_items(int64_t, int64_t) { return 32; }   // one 32-pair MFMA tile per wave and slice
 
 GArgs gargs(const nais_params_t* p, const nais_train_side_t* side, const int64_t* hist, int64_t n,
             const int64_t* target, int64_t b, float dropout_p, uint64_t seed) {
@@ -1301,21 +1421,25 @@ size_t g_workspace(int64_t b, int64_t n) {
 
 int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
   const size_t lds = g_lds_bytes(a, false);
-  static bool once = (set_lds(g_forward_kernel, 160 * 1024), true);
+  static bool once = (set_lds(gm_forward_kernel<4>, 160 * 1024), set_lds(gm_forward_kernel<2>, 160 * 1024), true);
   (void)once;
-  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + a.js - 1) / a.js));
-  hipLaunchKernelGGL(g_forward_kernel, grid, dim3(GW * 64), lds, st, a, Sp, Np);
-  return nais_internal_check_launch("g_forward_kernel");
+  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+  if (a.H > 64) hipLaunchKernelGGL(gm_forward_kernel<4>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
+  else hipLaunchKernelGGL(gm_forward_kernel<2>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
+  return nais_internal_check_launch("gm_forward_kernel");
 }
 
 int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
-               const GGrads& g, hipStream_t st) {
+               const GGrads& g, hipStream_t st, const int32_t* bad_rows = nullptr) {
   const size_t lds = g_lds_bytes(a, true);
-  static bool once = (set_lds(g_backward_kernel, 160 * 1024), true);
+  static bool once = (set_lds(gm_backward_kernel<4>, 160 * 1024), set_lds(gm_backward_kernel<2>, 160 * 1024), true);
   (void)once;
-  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + a.js - 1) / a.js));
-  hipLaunchKernelGGL(g_backward_kernel, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g);
-  return nais_internal_check_launch("g_backward_kernel");
+  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+  if (a.H > 64)
+    hipLaunchKernelGGL(gm_backward_kernel<4>, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g, bad_rows);
+  else
+    hipLaunchKernelGGL(gm_backward_kernel<2>, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g, bad_rows);
+  return nais_internal_check_launch("gm_backward_kernel");
 }
 
 }  // namespace
@@ -1324,7 +1448,7 @@ extern "C" {
 
 size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0) return 0;
-  return nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);
+  return nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);   // fast or general
 }
 
 int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
@@ -1332,9 +1456,12 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
                         int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
                         int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
                         void* stream) {
-  TShape sh;
-  int rc = tvalidate(params, &sh);
+  TShape sh{0, 0};
+  const bool fast = params && fast_ok(params);
+  int rc = fast ? tvalidate(params, &sh) : gvalidate(params, nullptr, b, n);
   if (rc) return rc;
+  if (params->variant != NAIS_VARIANT_BASIC)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "nais_train_step: NAIS_basic only (use nais_train_*_ex)");
   if ((rc = check_batch(hist, n, target, b))) return rc;
   if (!(dropout_p >= 0.f && dropout_p <= 1.f))
     return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
@@ -1358,15 +1485,25 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
   const int D = params->embed_dim, H = params->hidden;
   int64_t ns = 0, rb = (b + TROWS - 1) / TROWS;
   int js = 1;
+  GArgs ga{};
   if (n > 0) {
-    js = slice_items(b, n, FWD_PER_CU);
+    if (fast) {
+      js = slice_items(b, n, FWD_PER_CU);
+    } else {
+      ga = gargs(params, nullptr, hist, n, target, b, dropout_p, seed);
+      js = ga.js;
+    }
     ns = (n + js - 1) / js;
     if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
   }
   const TrainArgs a = targs(params, hist, n, target, b, js, dropout_p, seed);
   // 1. forward partials, 2. loss + dL/dpred
   if (n > 0) {
-    NAIS_TRAIN_DISPATCH(launch_train_forward, sh, a, part, part + ns * b, st);
+    if (fast) {
+      NAIS_TRAIN_DISPATCH(launch_train_forward, sh, a, part, part + ns * b, st);
+    } else {
+      rc = g_forward(ga, part, part + ns * b, st);
+    }
     if (rc) return rc;
   }
   hipLaunchKernelGGL(train_loss_kernel, dim3((unsigned)((b + 255) / 256)), dim3(256), 0, st,
@@ -1374,7 +1511,12 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
                      loss_sum, bad_rows);
   if ((rc = nais_internal_check_launch("train_loss_kernel"))) return rc;
   // 3. backward partials, 4. reduce into the zero-maintained gradient scratch
-  if (n > 0) {
+  if (n > 0 && !fast) {   // general kernels add straight into the scratch
+    float* gs = opt->grad_small;
+    const GGrads g{opt->grad_embed_history, opt->grad_embed_target, nullptr, gs,
+                   gs + int64_t(H) * D, gs + int64_t(H) * D + H, nullptr, nullptr};
+    if ((rc = g_backward(ga, saved, pred, gpred, g, st, bad_rows))) return rc;
+  } else if (n > 0) {
     float* Wt = part;
     float* Ww = Wt + ns * b * D;
     float* Wh = Ww + ns * rb * (int64_t(H) * D + 2 * H);

@@ -307,10 +307,11 @@ def test_make_batch_negatives_uniform():
     assert np.abs(first / (trials / n) - 1).max() < 0.15, first      # shuffled history order
 
 
-def test_fused_step_matches_dropin():
+@pytest.mark.parametrize("D,H", [(64, 64), (128, 128)])   # fused MFMA kernels / general kernels
+def test_fused_step_matches_dropin(D, H):
     """NAISTrainer.step == forward + BCELoss + backward + optim.Adagrad (same batch, same dropout)."""
     from poi_recommendation_models_amd import optim
-    P, D, H, n = 3000, 64, 64, 60
+    P, n = 3000, 60
     p = _params(P, D, H, 5)
     X = _csr(4, P, 80, seed=9)
     ma, mb = _model(p, drop_p=0.5), _model(p, drop_p=0.5)
@@ -338,8 +339,9 @@ def test_fused_step_matches_dropin():
 
 
 @pytest.mark.parametrize("wd", [0.0, 0.01])
-def test_fused_step_oracle(wd):
-    P, D, H, n = 2000, 32, 48, 40
+@pytest.mark.parametrize("D,H", [(32, 48), (128, 128), (80, 72)])
+def test_fused_step_oracle(wd, D, H):
+    P, n = 2000, 40
     p = _params(P, D, H, 6)
     X = _csr(2, P, 10, seed=1)
     m = _model(p)
@@ -356,8 +358,9 @@ def test_fused_step_oracle(wd):
         assert bad.mean() <= 1e-3, (k, int(bad.sum()))
 
 
-def test_fused_nan_batch_skips_update():
-    P, D, H = 500, 16, 16
+@pytest.mark.parametrize("D,H", [(16, 16), (128, 128)])
+def test_fused_nan_batch_skips_update(D, H):
+    P = 500
     p = _params(P, D, H, 8)
     X = _csr(2, P, 5, seed=2)
     m = _model(p)
