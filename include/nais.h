@@ -395,14 +395,16 @@ int32_t nais_dropout_mask(uint64_t seed, int64_t b, int64_t n, int32_t hidden, f
 
 /*
  * The same training forward / backward for every NAIS variant (NAIS_basic, NAIS_regionEmbedding,
- * NAIS_region_distance_Embedding; run.py:91-280) and any embed_dim / hidden up to 128 (run.py's
+ * NAIS_region_distance_Embedding, NAIS_distance_Embedding; run.py:91-280, 365-430) and any
+ * embed_dim / hidden up to 128 (run.py's
  * defaults are factor_num = hidden_dim = 128). NAIS_basic at embed_dim in {8,16,32,64}, hidden <= 64
  * runs the fused MFMA kernels above; everything else a general kernel with the same math and the
  * same dropout draws. The region variants read full rows [embed_history | embed_region[region]]:
  *   side->hist_region [n], side->target_region [b]  (regions of the history items / target rows,
  *   get_NAIS_batch_region, batches.py:67-108); region_distance also side->target_lat_long
  *   [b, n, 2] f32, row stride latlon_ld (run.py:240-245), x100 before dist_layer (model.py:265).
- * NAIS_region_distance_Embedding has no dropout (model.py:268): pass dropout_p = 0.
+ * NAIS_distance_Embedding reads basic rows and side->target_lat_long (x1000, model.py:369).
+ * The two distance variants have no dropout (model.py:268, 369-371): pass dropout_p = 0.
  * Gradients are ADDED into grads (dense, fp32 atomics for repeated ids); embed_region and
  * dist_w / dist_b are required for the variants that have them. nais_train_forward / _backward
  * above are these with side = NULL (NAIS_basic only). Workspace: nais_train_workspace_size().

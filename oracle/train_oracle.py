@@ -35,11 +35,12 @@ def train_step_basic(p, hist, data, labels, beta=0.5, keep=None, drop_p=0.0):
 
 
 def train_step(p, hist, data, labels, hist_region=None, data_region=None, latlon=None, beta=0.5,
-               keep=None, drop_p=0.0):
+               keep=None, drop_p=0.0, dist_scale=100.0):
     """Forward + backward of NAIS_basic, NAIS_regionEmbedding (model.py:144-180: rows
     [E_hist | E_reg[region]] against [E_tgt | E_reg[region]], when `hist_region` / `data_region`
     are given) or NAIS_region_distance_Embedding (model.py:246-297: also the distance feature
-    sigmoid(dist_layer(100 * latlon)) appended to h (.) t, when `latlon` [b, n, 2] is given)."""
+    sigmoid(dist_layer(100 * latlon)) appended to h (.) t, when `latlon` [b, n, 2] is given), or
+    NAIS_distance_Embedding (model.py:355-395: `latlon` without regions, dist_scale = 1000)."""
     EH = np.asarray(p["embed_history.weight"], F64)
     ET = np.asarray(p["embed_target.weight"], F64)
     W1 = np.asarray(p["attn_layer1.weight"], F64)
@@ -64,7 +65,7 @@ def train_step(p, hist, data, labels, hist_region=None, data_region=None, latlon
     if latlon is not None:                              # model.py:265-267
         Wd = np.asarray(p["dist_layer.weight"], F64)
         bd = np.asarray(p["dist_layer.bias"], F64)
-        ll = np.asarray(latlon, F64) * 100.0
+        ll = np.asarray(latlon, F64) * dist_scale         # x100 (:265) / x1000 (:369)
         feat = 1.0 / (1.0 + np.exp(-(ll @ Wd.T + bd)))   # sigmoid(dist_layer(100 ll))
         x = np.concatenate([x, feat], -1)
     u = x @ W1.T + b1                                   # model.py:71 attn_layer1

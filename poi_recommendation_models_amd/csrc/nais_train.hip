@@ -1373,8 +1373,14 @@ int gvalidate(const nais_params_t* p, const nais_train_side_t* side, int64_t b, 
         return nais_internal_fail(NAIS_E_INVALID, "region_distance needs side->target_lat_long [b, n, 2]");
       break;
     }
+    case NAIS_VARIANT_DISTANCE:
+      if (p->item_dim != D || p->din != D + 2 || !p->dist_w || !p->dist_b)
+        return nais_internal_fail(NAIS_E_INVALID, "distance: item_dim == embed_dim, din == embed_dim + 2, dist_layer set");
+      if (b > 0 && n > 0 && (!side || !side->target_lat_long || side->latlon_ld < 2 * n))
+        return nais_internal_fail(NAIS_E_INVALID, "distance needs side->target_lat_long [b, n, 2]");
+      break;
     default:
-      return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: variant must be basic, region or region_distance");
+      return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: unknown variant");
   }
   return NAIS_OK;
 }
@@ -1401,13 +1407,14 @@ GArgs gargs(const nais_params_t* p, const nais_train_side_t* side, const int64_t
   a.b = b;
   a.n = n;
   a.D = p->embed_dim;
-  a.IDIM = p->variant == NAIS_VARIANT_BASIC ? p->embed_dim : p->item_dim;
-  a.RDIM = p->variant == NAIS_VARIANT_BASIC ? 0 : p->region_dim;
+  const bool reg = p->variant == NAIS_VARIANT_REGION || p->variant == NAIS_VARIANT_REGION_DISTANCE;
+  a.IDIM = reg ? p->item_dim : p->embed_dim;
+  a.RDIM = reg ? p->region_dim : 0;
   a.H = p->hidden;
   a.DIN = p->din;
   a.variant = p->variant;
   a.beta = p->beta;
-  a.dscale = 100.f;   // model.py:265
+  a.dscale = p->variant == NAIS_VARIANT_DISTANCE ? 1000.f : 100.f;   // model.py:369 / :265
   a.js = g_slice_items(b, n);
   a.drop = make_drop(dropout_p, seed);
   return a;
@@ -1645,10 +1652,13 @@ int32_t nais_train_backward_ex(const nais_params_t* params, const nais_train_sid
   if (!pred || !saved || !grad_pred || !grads->embed_history || !grads->embed_target || !grads->w1 ||
       !grads->b1 || !grads->w2)
     return nais_internal_fail(NAIS_E_INVALID, "missing pred/saved/grad pointer");
-  if (params->variant != NAIS_VARIANT_BASIC && !grads->embed_region)
+  if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
+      !grads->embed_region)
     return nais_internal_fail(NAIS_E_INVALID, "region variants need grads->embed_region");
   if (params->variant == NAIS_VARIANT_REGION_DISTANCE && (!grads->dist_w || !grads->dist_b))
     return nais_internal_fail(NAIS_E_INVALID, "region_distance needs grads->dist_w / dist_b");
+  if (params->variant == NAIS_VARIANT_DISTANCE && (!grads->dist_w || !grads->dist_b))
+    return nais_internal_fail(NAIS_E_INVALID, "distance needs grads->dist_w / dist_b");
   (void)workspace;
   (void)workspace_bytes;
   const GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);

@@ -129,11 +129,10 @@ class _NAISDevice(nn.Module):
     def _run_forward(self, history, target, history_region=None, target_region=None,
                      target_lat_long=None, sigmoid=True):
         if self.training:
-            if not sigmoid or self.VARIANT == _capi.VARIANT_DISTANCE:
+            if not sigmoid:
                 raise NotImplementedError(
-                    f"{type(self).__name__}: training-mode {'forward' if sigmoid else 'attention_network'}"
-                    " is implemented for NAIS_basic / NAIS_regionEmbedding / NAIS_region_distance_Embedding"
-                    ".forward (SURVEY.md 8(f1)); call model.eval()")
+                    f"{type(self).__name__}: training-mode attention_network is not implemented; the "
+                    "training path is the forward (SURVEY.md 8(f1)); call model.eval()")
             return self._train_forward(history, target, history_region, target_region, target_lat_long)
         dev = self._check_device(history, target, history_region, target_region, target_lat_long)
         if history.dim() != 2 or target.dim() != 1 or history.shape[0] != target.shape[0]:
@@ -192,7 +191,7 @@ class _NAISDevice(nn.Module):
         if self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE):
             names.append("embed_region")
         names += ["w1", "b1", "w2"]
-        if self.VARIANT == _capi.VARIANT_REGION_DISTANCE:
+        if self.VARIANT in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE):
             names += ["dist_w", "dist_b"]
         return names
 
@@ -239,7 +238,14 @@ class _NAISDevice(nn.Module):
                     ll = ll.contiguous()
             hreg = history_region[0].contiguous() if b > 0 else history_region.new_empty(0)
             side = (hreg, target_region.to(torch.int64).contiguous(), ll)
-        drop = getattr(self, "drop", None)        # none in NAIS_region_distance_Embedding (model.py:268)
+        elif self.VARIANT == _capi.VARIANT_DISTANCE:
+            if target_lat_long is None or tuple(target_lat_long.shape) != (b, n, 2):
+                raise ValueError("target_lat_long must be [b, n, 2]")
+            ll = target_lat_long.to(torch.float32)
+            if not (ll.stride(2) == 1 and ll.stride(1) == 2):
+                ll = ll.contiguous()
+            side = (None, None, ll)
+        drop = getattr(self, "drop", None)        # none in the two distance variants (model.py:268, 369)
         p = float(drop.p) if drop is not None and drop.training else 0.0
         seed = int(torch.randint(0, 2**62, (1,)).item())   # torch's CPU generator: manual_seed applies
         pred, nan = _NAISTrainStep.apply(self, hist, target, p, seed, side, *self._train_params())

@@ -10,6 +10,8 @@ train_step_region.npz  one get_NAIS_batch_region-shaped batch (batches.py:67-108
       region_distance/  NAIS_region_distance_Embedding(P, 32, 24, 0.5, R, 1) with
                         target_lat_long = latlon_mat[target, history] (run.py:240-245)
       basic128/         NAIS_basic(P, 128, 128, 0.5): run.py's default factor_num = hidden_dim
+      distance/         NAIS_distance_Embedding(P, 32, 24, 0.5, R, 1) (model.py:306-408), latlon
+                        from a 20x tighter box (x1000 would saturate the sigmoid)
     <case>/p/<param>, <case>/grad/<param>, hist, data, labels, hist_region, data_region, latlon,
     pred, loss.
 """
@@ -39,7 +41,8 @@ def main(ref_path="/root/reference"):
     out = {"coords": coords, "region_of": region_of}
     cases = (("region", lambda: model.NAIS_regionEmbedding(P, 32, 24, 0.5, R)),
              ("region_distance", lambda: model.NAIS_region_distance_Embedding(P, 32, 24, 0.5, R, 1)),
-             ("basic128", lambda: model.NAIS_basic(P, 128, 128, 0.5)))
+             ("basic128", lambda: model.NAIS_basic(P, 128, 128, 0.5)),
+             ("distance", lambda: model.NAIS_distance_Embedding(P, 32, 24, 0.5, R, 1)))
     for ci, (case, make) in enumerate(cases):
         m = make()
         p = random_state(m, 300 + ci, 0.3, 0.1)
@@ -53,10 +56,12 @@ def main(ref_path="/root/reference"):
         hist = np.repeat(positives.reshape(1, -1), len(data_), 0)
         hreg, dreg = region_of[hist], region_of[data_]
         latlon = np.abs(coords[data_][:, None, :] - coords[hist]).astype(np.float32)   # run.py:47-54
+        if case == "distance":    # x1000 saturates the sigmoid at city scale: a tighter box
+            latlon = (latlon * 0.05).astype(np.float32)
         args = [torch.from_numpy(hist), torch.from_numpy(data_)]
         if case != "basic128":
             args += [torch.from_numpy(hreg), torch.from_numpy(dreg)]
-        if case == "region_distance":
+        if case in ("region_distance", "distance"):
             args.append(torch.from_numpy(latlon))
         pred = m(*args)
         loss = m.loss_func(pred, torch.tensor(labels, dtype=torch.float32))

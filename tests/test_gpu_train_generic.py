@@ -36,6 +36,8 @@ def _make(case, p, drop_p=0.0):
     H, din = p["attn_layer1.weight"].shape
     if case == "basic":
         m = M.NAIS_basic(P, I, H, 0.5)
+    elif case == "distance":
+        m = M.NAIS_distance_Embedding(P, I, H, 0.5, 10, 1)
     elif case == "region":
         m = M.NAIS_regionEmbedding(P, din, H, 0.5, p["embed_region.weight"].shape[0])
     else:
@@ -56,7 +58,7 @@ def _step(m, case, hist, data, labels, hreg=None, dreg=None, latlon=None):
     args = [_t(hist), _t(data)]
     if case != "basic":
         args += [_t(hreg), _t(dreg)]
-    if case == "region_distance":
+    if case in ("region_distance", "distance"):
         args.append(_t(latlon))
     pred = m(*args)
     loss = m.loss_func(pred, _t(labels))
@@ -73,7 +75,7 @@ def _assert_grads(got, ref, rtol=GRAD_RTOL):
         assert np.abs(got[k] - r).max() / scale <= rtol, (k, np.abs(got[k] - r).max() / scale)
 
 
-@pytest.mark.parametrize("case", ["region", "region_distance", "basic128"])
+@pytest.mark.parametrize("case", ["region", "region_distance", "basic128", "distance"])
 def test_train_generic_golden(case):
     z = load_golden("train_step_region.npz")
     pre = case + "/"
@@ -99,16 +101,16 @@ def _mask(seed, b, n, H, p):
 def _params(case, P, R, D, H, seed):
     r = np.random.default_rng(seed)
     f = np.float32
-    I = D if case == "basic" else D // 2
-    din = D + 2 if case == "region_distance" else D
+    I = D if case in ("basic", "distance") else D // 2
+    din = D + 2 if case in ("region_distance", "distance") else D
     p = {"embed_history.weight": r.normal(0, 0.3, (P, I)).astype(f),
          "embed_target.weight": r.normal(0, 0.3, (P, I)).astype(f),
          "attn_layer1.weight": r.uniform(-din ** -0.5, din ** -0.5, (H, din)).astype(f),
          "attn_layer1.bias": r.normal(0, 0.1, H).astype(f),
          "attn_layer2.weight": r.uniform(-H ** -0.5, H ** -0.5, (1, H)).astype(f)}
-    if case != "basic":
+    if case in ("region", "region_distance"):
         p["embed_region.weight"] = r.normal(0, 0.3, (R, D // 2)).astype(f)
-    if case == "region_distance":
+    if case in ("region_distance", "distance"):
         p["dist_layer.weight"] = r.uniform(-0.7, 0.7, (2, 2)).astype(f)
         p["dist_layer.bias"] = r.normal(0, 0.1, 2).astype(f)
     return p
@@ -122,6 +124,8 @@ def _params(case, P, R, D, H, seed):
     ("region", 128, 128, 12, 0.5),
     ("region_distance", 64, 48, 25, 0.0),   # no dropout in this model (model.py:268)
     ("region_distance", 128, 128, 8, 0.0),
+    ("distance", 64, 64, 20, 0.0),          # NAIS_distance_Embedding (x1000, no dropout)
+    ("distance", 128, 100, 11, 0.0),
 ])
 def test_train_generic_oracle(case, D, H, n, drop, monkeypatch):
     P, R = 3000, 40
@@ -134,17 +138,19 @@ def test_train_generic_oracle(case, D, H, n, drop, monkeypatch):
     hist = np.repeat(pos.reshape(1, -1), len(data), 0)
     region_of = r.integers(0, R, P)
     hreg, dreg = region_of[hist], region_of[data]
-    latlon = r.uniform(0, 0.05, (len(data), n, 2)).astype(np.float32)
+    latlon = r.uniform(0, 0.05 if case != "distance" else 0.003, (len(data), n, 2)).astype(np.float32)
     m = _make(case, p, drop)
     seed = 123456789 + n
     monkeypatch.setattr(torch, "randint", lambda *a, **k: torch.tensor([seed]))
     pred, loss, grads = _step(m, case, hist, data, labels, hreg, dreg, latlon)
     keep = _mask(seed, len(data), n, H, drop) if drop > 0 else None
     kw = {}
-    if case != "basic":
+    if case in ("region", "region_distance"):
         kw.update(hist_region=hreg, data_region=dreg)
-    if case == "region_distance":
+    if case in ("region_distance", "distance"):
         kw["latlon"] = latlon
+    if case == "distance":
+        kw["dist_scale"] = 1000.0
     ref = train_oracle.train_step(p, hist, data, labels, keep=keep, drop_p=drop, **kw)
     assert np.max(np.abs(pred - ref["pred"])) <= SCORE_ATOL
     assert abs(loss - ref["loss"]) <= 1e-5

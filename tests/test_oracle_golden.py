@@ -255,7 +255,7 @@ def test_forward_disentangled(tag, n):
     assert np.array_equal(mine, dist)
 
 
-@pytest.mark.parametrize("case", ["region", "region_distance", "basic128"])
+@pytest.mark.parametrize("case", ["region", "region_distance", "basic128", "distance"])
 def test_train_oracle_region_variants_match_reference(case):
     """The training restatement for NAIS_regionEmbedding / NAIS_region_distance_Embedding and
     NAIS_basic at run.py's default D = H = 128 vs the reference's autograd
@@ -265,10 +265,12 @@ def test_train_oracle_region_variants_match_reference(case):
     pre = case + "/"
     p = {k[len(pre) + 2:]: z[k] for k in z.files if k.startswith(pre + "p/")}
     kw = {}
-    if case != "basic128":
+    if case in ("region", "region_distance"):
         kw.update(hist_region=z[pre + "hist_region"], data_region=z[pre + "data_region"])
-    if case == "region_distance":
+    if case in ("region_distance", "distance"):
         kw["latlon"] = z[pre + "latlon"]
+    if case == "distance":
+        kw["dist_scale"] = 1000.0
     r = train_oracle.train_step(p, z[pre + "hist"], z[pre + "data"], z[pre + "labels"], **kw)
     assert np.max(np.abs(r["pred"] - z[pre + "pred"])) <= 1e-6
     assert abs(r["loss"] - float(z[pre + "loss"])) <= 1e-6
