@@ -1175,8 +1175,9 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // ---------------------------------------------------------------------------------------------
 // Top-k per user (validation.py:26-27): exact radix select on 64-bit keys
 //   key = ordered(score) << 32 | (0xFFFFFFFF - poi)   -> unique; larger key = (higher score, lower id)
-// 8 MSB-first 8-bit passes over the user's score row (L2-resident), then the k winners are
-// collected and bitonic-sorted in LDS. NaN (canonical, positive) orders above +inf.
+// MSB-first 8-bit passes over the user's score row until the keys at or above the selected prefix
+// fit a 4096-key LDS buffer (typically 2 passes), then those keys are collected and bitonic-sorted
+// in LDS and the first k kept. NaN (canonical, positive) orders above +inf.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t ord_f32(float f) {
   uint32_t u = __float_as_uint(f);
@@ -1186,29 +1187,66 @@ __device__ __forceinline__ float unord_f32(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
+// Visit (c, score) for every c in [0, P): 16-byte loads when the row is 16-byte aligned.
+template <class F>
+__device__ __forceinline__ void topk_visit(const float* __restrict__ s, int64_t P, F&& f) {
+  const int tid = threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {
+    const int64_t P4 = P >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(s);
+#pragma unroll 2
+    for (int64_t q = tid; q < P4; q += TOPK_THREADS) {
+      const float4 v = s4[q];
+      f(4 * q, v.x);
+      f(4 * q + 1, v.y);
+      f(4 * q + 2, v.z);
+      f(4 * q + 3, v.w);
+    }
+    for (int64_t c = 4 * P4 + tid; c < P; c += TOPK_THREADS) f(c, s[c]);
+  } else {
+    for (int64_t c = tid; c < P; c += TOPK_THREADS) f(c, s[c]);
+  }
+}
+
+// LDS histogram add with the wave's most common bin (the first active lane's) added once by one
+// lane: score rows cluster in a few top digits, and same-address LDS atomics serialise.
+__device__ __forceinline__ void topk_hist_add(uint32_t* hist, bool pred, uint32_t bin) {
+  const unsigned long long act = __ballot(pred);
+  if (!act) return;
+  const int leader = __ffsll((long long)act) - 1;
+  const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, leader);
+  const unsigned long long same = __ballot(pred && bin == b0);
+  if ((int)(threadIdx.x & 63) == leader) atomicAdd(&hist[b0], (uint32_t)__popcll(same));
+  else if (pred && bin != b0) atomicAdd(&hist[bin], 1u);
+}
+
+constexpr int TOPK_CAP = 4096;   // keys collected for the final sort (32 KiB of LDS)
+
 __global__ void __launch_bounds__(TOPK_THREADS)
 topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k,
             int32_t* __restrict__ out_ids, float* __restrict__ out_scores,
             int32_t* __restrict__ short_count) {
   __shared__ uint32_t hist[256];
-  __shared__ unsigned long long buf[MAX_K];
-  __shared__ uint32_t sh_bin, sh_above, sh_total, sh_cnt;
+  __shared__ unsigned long long buf[TOPK_CAP];
+  __shared__ uint32_t sh_bin, sh_above, sh_binc, sh_total, sh_cnt;
   const float* s = scores + (int64_t)blockIdx.x * score_ld;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long prefix = 0, mask = 0;
-  uint32_t rem = (uint32_t)k;
+  uint32_t rem = (uint32_t)k, above_total = 0, n_collect = 0;
   int kk = k;
+  // MSB-first 8-bit digits of the 64-bit key; stop as soon as the keys at or above the selected
+  // digit prefix (the k winners plus the rest of their bin) fit the collect buffer -- usually
+  // after the second digit -- so a row is read 3 times instead of 9.
   for (int pass = 0; pass < 8; ++pass) {
     const int shift = 56 - 8 * pass;
     if (tid < 256) hist[tid] = 0;
     __syncthreads();
-    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
-      float v = s[c];
-      if (v < 0.f) continue;  // history POI (or padding): not a candidate
+    topk_visit(s, P, [&](int64_t c, float v) {
+      const bool cand = !(v < 0.f);   // history POI (or padding) = -1: not a candidate
       const unsigned long long key =
           ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)c);
-      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-    }
+      topk_hist_add(hist, cand && (key & mask) == prefix, (uint32_t)(key >> shift) & 255u);
+    });
     __syncthreads();
     if (wave == 0) {
       const int base = 255 - lane * 4;
@@ -1228,14 +1266,16 @@ topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k
       if (need > 0 && excl < need && incl >= need) {
         uint32_t cum = excl;
         int bsel;
-        if (cum + c0 >= need) bsel = base;
-        else if ((cum += c0) + c1 >= need) bsel = base - 1;
-        else if ((cum += c1) + c2 >= need) bsel = base - 2;
-        else { cum += c2; bsel = base - 3; }
+        uint32_t bc;
+        if (cum + c0 >= need) { bsel = base; bc = c0; }
+        else if ((cum += c0) + c1 >= need) { bsel = base - 1; bc = c1; }
+        else if ((cum += c1) + c2 >= need) { bsel = base - 2; bc = c2; }
+        else { cum += c2; bsel = base - 3; bc = c3; }
         sh_bin = (uint32_t)bsel;
         sh_above = cum;
+        sh_binc = bc;
       }
-      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; }
+      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; sh_binc = 0; }
     }
     __syncthreads();
     if (pass == 0) {
@@ -1245,29 +1285,32 @@ topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k
     prefix |= (unsigned long long)sh_bin << shift;
     mask |= 255ull << shift;
     rem -= sh_above;
+    above_total += sh_above;
+    n_collect = above_total + sh_binc;   // keys >= prefix
     __syncthreads();
+    if (kk == 0 || n_collect <= (uint32_t)TOPK_CAP) break;   // block-uniform
   }
   if (tid == 0) sh_cnt = 0;
   __syncthreads();
   if (kk > 0) {
-    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
-      float v = s[c];
-      if (v < 0.f) continue;
+    topk_visit(s, P, [&](int64_t c, float v) {
+      if (v < 0.f) return;
       const unsigned long long key =
           ((unsigned long long)ord_f32(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)c);
       if (key >= prefix) {
         const uint32_t pos = atomicAdd(&sh_cnt, 1u);
-        if (pos < (uint32_t)MAX_K) buf[pos] = key;
+        if (pos < (uint32_t)TOPK_CAP) buf[pos] = key;
       }
-    }
+    });
+  } else {
+    n_collect = 0;
   }
   __syncthreads();
   int n2 = 1;
-  while (n2 < k) n2 <<= 1;
-  for (int i = tid; i < n2; i += TOPK_THREADS)
-    if (i >= kk) buf[i] = 0ull;
+  while (n2 < (int)n_collect || n2 < k) n2 <<= 1;
+  for (int i = (int)n_collect + tid; i < n2; i += TOPK_THREADS) buf[i] = 0ull;   // keys > 0
   __syncthreads();
-  // bitonic sort, descending
+  // bitonic sort, descending; keys are unique, so the order is (score desc, id asc)
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = tid; i < n2; i += TOPK_THREADS) {
