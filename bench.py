@@ -337,15 +337,22 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         catalog.PAIR_CU_LAYOUT = os.environ["NAIS_PAIR_CU_LAYOUT"]
     if os.environ.get("NAIS_PAIR_BLOCK_COLS"):
         catalog.PAIR_BLOCK_COLS = int(os.environ["NAIS_PAIR_BLOCK_COLS"])
+    if os.environ.get("NAIS_PAIR_FIRST_TABLE_ALL_CUS"):
+        catalog.PAIR_FIRST_TABLE_ALL_CUS = os.environ["NAIS_PAIR_FIRST_TABLE_ALL_CUS"] == "1"
+    # NAIS_EMULATE_WORLD=N (one process): time rank 0's column shard of an N-GPU run (its tables,
+    # gathers and local top-k; no collective) -- per-rank cost and strong-scaling headroom on one GPU
+    emulate = int(os.environ.get("NAIS_EMULATE_WORLD", "1"))
     P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
     users = np.arange(a.num_users)
     group = None
     if world == 1:   # the same code path with a trivial process group is not needed: call direct
         from poi_recommendation_models_amd.catalog import _score_topk_pairs
 
+        S_em = (a.num_pois + emulate - 1) // emulate
+
         def job(events=None):
             return _score_topk_pairs(model, csr, users, K, None, None, None, None, force=True,
-                                     events=events)
+                                     events=events, cols=(0, S_em) if emulate > 1 else None)
     else:
         def job(events=None):
             return distributed_topk_pairs(model, csr, users, K, group=group, events=events)
@@ -378,6 +385,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         elapsed = float(t.item())
     pairs_job = float((P - hist_len[users]).sum())            # every user's whole catalog
     S = (P + world - 1) // world
+    if emulate > 1 and world == 1:
+        S = (P + emulate - 1) // emulate
+        pairs_job /= emulate     # ~ the shard's share (value is then a per-rank rate estimate)
     c0, c1 = min(rank * S, P), min((rank + 1) * S, P)
     NC = c1 - c0
     entries = int(hist_len.sum())
@@ -396,7 +406,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     traffic = None
     try:
         tj = json.load(open(a.traffic_json)).get("pairs_gather", {})
-        if tj.get("num_users") == a.num_users and tj.get("num_pois") == P and tj.get("world") == world:
+        if (tj.get("num_users") == a.num_users and tj.get("num_pois") == P and tj.get("world") == world
+                and tj.get("block_cols") == catalog.PAIR_BLOCK_COLS):
             traffic = tj.get("hbm_bytes_per_launch")
     except Exception:
         pass
@@ -433,6 +444,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "model": "NAIS_basic", "strategy": "pairs", "num_users": a.num_users, "num_pois": P,
                 "table_cus": catalog.PAIR_TABLE_CUS, "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
+                "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
+                **({"emulated_world_shard": emulate} if emulate > 1 and world == 1 else {}),
                 "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,
                 "pairs_per_step": pairs_job, "history_entries": entries, "distinct_history_pois": J,
                 "parallelism": f"POI columns sharded over {world} GPU(s) (all users per rank), "

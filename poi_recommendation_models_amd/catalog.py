@@ -193,8 +193,10 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
 
 # Column-block width of the pair tables. Serial (profiles/r1/pairs/): 8192 best of 1024 / 8192 /
 # 100000. Overlapped (below; profiles/r1/overlap/): 1024 / 2048 / 3072 / 4096 / 8192 columns ->
-# 606 / 610 / 619 / 627 / 665 ms per config-4 step (a shorter pipeline fill).
-PAIR_BLOCK_COLS = 2048
+# 606 / 610 / 619 / 627 / 665 ms per config-4 step (a shorter pipeline fill). With block 0's table
+# on every CU (profiles/r1/blocks/): 1024 vs 2048 -> 579.8 vs 581.3 ms at N = 1, and on one rank's
+# column shard of an 8-GPU run (12.5k columns) 512 / 1024 / 2048 -> 77.2 / 77.7 / 79.9 ms.
+PAIR_BLOCK_COLS = 1024
 # Table (MFMA-bound) and gather (HBM-bound) phases of consecutive column blocks run side by side
 # on CU-masked streams: tables on CUs [0, PAIR_TABLE_CUS), gathers on the rest (-1 = half the
 # device's CUs, i.e. 4 of the 8 XCDs each; 0 = serial on the caller's stream). Double-buffered
@@ -203,6 +205,7 @@ PAIR_BLOCK_COLS = 2048
 # boundaries lose; masks that interleave CU ids are not honoured -- both kernels then share
 # every CU).
 PAIR_TABLE_CUS = -1
+PAIR_FIRST_TABLE_ALL_CUS = True   # block 0's table (nothing to overlap it with) on every CU
 PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 _masked: dict = {}
 
@@ -324,6 +327,12 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     for _ in range(2 if overlap else 1)]
             if overlap:
                 ts, gs = _masked_streams(dev, table_cus)
+                first_all = PAIR_FIRST_TABLE_ALL_CUS
+                if first_all:      # block 0's table alone, on the caller's stream (all CUs)
+                    w0 = min(W, c1_all - blocks[0])
+                    timed("table", lambda: model._pair_table(lib, prm, items, J, blocks[0], w0, reg, cor, llm,
+                                                             tabs[0][0].data_ptr(), tabs[0][1].data_ptr(),
+                                                             W, st))
                 ts.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
                 done_g = [None, None]
@@ -333,12 +342,15 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 if overlap:
                     if done_g[b % 2] is not None:
                         ts.wait_event(done_g[b % 2])     # buffer free: its gather finished
-                    e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e_t0.record(ts)
-                    model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
-                                      tab[1].data_ptr(), W, ts.cuda_stream)
-                    e_t1.record(ts)
-                    gs.wait_event(e_t1)
+                    if not (b == 0 and first_all):
+                        e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e_t0.record(ts)
+                        model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
+                                          tab[1].data_ptr(), W, ts.cuda_stream)
+                        e_t1.record(ts)
+                        gs.wait_event(e_t1)
+                        if events is not None:
+                            events.append(("table", e_t0, e_t1))
                     e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e_g0.record(gs)
                     _capi.check(lib.nais_pair_gather(
@@ -349,7 +361,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     e_g1.record(gs)
                     done_g[b % 2] = e_g1
                     if events is not None:
-                        events += [("table", e_t0, e_t1), ("gather", e_g0, e_g1)]
+                        events.append(("gather", e_g0, e_g1))
                     continue
                 timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
                                                          tab[0].data_ptr(), tab[1].data_ptr(), W, st))

@@ -70,6 +70,15 @@ struct DevParams {
 //   e = exp(a) * [item != c]  to e[r * ld + c - col0]   and   e * (h . t)  to es[...]
 // -- all a user needs from the pair: pair_gather_kernel sums them over each user's history rows.
 // e == nullptr: the normal per-user scoring.
+#ifndef NAIS_TABLE_NT
+#define NAIS_TABLE_NT 0
+#endif
+// pair-table stores (A/B knob: non-temporal, so the tables streaming out do not evict the
+// gather's stripe from the Infinity Cache)
+__device__ __forceinline__ void tab_store(float* p, float v) {
+  if (NAIS_TABLE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 struct TableOut {
   float* e = nullptr;
   float* es = nullptr;
@@ -377,8 +386,8 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
       if (tab.e) {
         if (valid && hh == 0) {
           const int64_t o = (hbeg + j0 + jj) * tab.ld + (c - tab.col0);
-          tab.e[o] = e;
-          tab.es[o] = e * s;
+          tab_store(tab.e + o, e);
+          tab_store(tab.es + o, e * s);
         }
         continue;
       }
@@ -1079,8 +1088,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       if (tab.e) {
         if (valid && hh == 0) {
           const int64_t o = (hbeg + j0 + pj) * tab.ld + (c - tab.col0);
-          tab.e[o] = e;
-          tab.es[o] = e * sv;
+          tab_store(tab.e + o, e);
+          tab_store(tab.es + o, e * sv);
         }
       } else {
         in_hist |= !keep;

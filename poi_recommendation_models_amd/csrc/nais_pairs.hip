@@ -26,14 +26,18 @@
 
 namespace {
 
-typedef float nf4 __attribute__((ext_vector_type(4)));
+#ifndef NAIS_GATHER_CPL
+#define NAIS_GATHER_CPL 4   // columns per lane: stripe = 64 * CPL columns (A/B knob)
+#endif
+constexpr int CPL = NAIS_GATHER_CPL;
+typedef float nfv __attribute__((ext_vector_type(CPL)));
 
 #ifndef NAIS_GATHER_NT
 #define NAIS_GATHER_NT 0   // 1: non-temporal table loads (slower: the Infinity Cache then holds nothing)
 #endif
-__device__ __forceinline__ nf4 load4(const float* p) {
-  if (NAIS_GATHER_NT) return __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
-  return *reinterpret_cast<const nf4*>(p);
+__device__ __forceinline__ nfv loadv(const float* p) {
+  if (NAIS_GATHER_NT) return __builtin_nontemporal_load(reinterpret_cast<const nfv*>(p));
+  return *reinterpret_cast<const nfv*>(p);
 }
 
 constexpr int SCAN_THREADS = 1024;
@@ -112,12 +116,15 @@ place_kernel(int32_t* __restrict__ flag_rowmap, int64_t P, const int32_t* __rest
   }
 }
 
-// One wave per user, 4 users per workgroup; a wave covers a 256-column stripe (4 columns per
-// lane). Grid x = user groups (fastest), y = stripes: the workgroups in flight read the same
+// One wave per user, 4 users per workgroup; a wave covers a 256-column stripe (CPL = 4 columns
+// per lane). Grid x = user groups (fastest), y = stripes: the workgroups in flight read the same
 // stripe of the tables -- J x 256 x 8 B, ~200 MB at J = 100k -- so the Infinity Cache serves the
 // rows the ~50 users sharing each item read (A/B: profiles/r1/pairs/). N and S are summed in
 // history (CSR) order, then the score of model.py:55 / validation.py:26; history POIs get -1.
-constexpr int GW = 4;                       // users (waves) per workgroup
+#ifndef NAIS_GATHER_GW
+#define NAIS_GATHER_GW 4
+#endif
+constexpr int GW = NAIS_GATHER_GW;          // users (waves) per workgroup
 
 // lane jj's 64-bit value, as a wave-uniform scalar (readlane returns int: widen via uint32_t)
 __device__ __forceinline__ int64_t bcast64(uint32_t lo, uint32_t hi, int jj) {
@@ -125,7 +132,7 @@ __device__ __forceinline__ int64_t bcast64(uint32_t lo, uint32_t hi, int jj) {
   const uint32_t h = uint32_t(__builtin_amdgcn_readlane(int(hi), jj));
   return int64_t((uint64_t(h) << 32) | uint64_t(l));
 }
-constexpr int STRIPE = 256;                 // columns per wave
+constexpr int STRIPE = 64 * CPL;             // columns per wave
 
 __global__ void __launch_bounds__(GW * 64)
 pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, int64_t ld,
@@ -139,9 +146,11 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
   if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
   const int64_t u = users[slot];
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
-  const int64_t x = int64_t(blockIdx.y) * STRIPE + lane * 4;   // column within the block
-  const bool full = x + 4 <= cols;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f;
+  const int64_t x = int64_t(blockIdx.y) * STRIPE + lane * CPL;   // column within the block
+  const bool full = x + CPL <= cols;
+  float Sa[CPL], Na[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) Sa[q] = Na[q] = 0.f;
   for (int64_t j0 = 0; j0 < hl; j0 += 64) {
     const int jn = (int)std::min<int64_t>(64, hl - j0);
     // row offsets of 64 history items, one per lane, broadcast with readlane below
@@ -151,28 +160,30 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
 #pragma unroll 8
       for (int jj = 0; jj < jn; ++jj) {
         const int64_t o = bcast64(mlo, mhi, jj) + x;
-        const nf4 e = load4(E + o);
-        const nf4 t = load4(ES + o);
-        s0 += e.x; s1 += e.y; s2 += e.z; s3 += e.w;
-        n0 += t.x; n1 += t.y; n2 += t.z; n3 += t.w;
+        const nfv e = loadv(E + o);
+        const nfv t = loadv(ES + o);
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+          Sa[q] += e[q];
+          Na[q] += t[q];
+        }
       }
     } else {
       for (int jj = 0; jj < jn; ++jj) {
         const int64_t o = bcast64(mlo, mhi, jj) + x;
-        if (x < cols) { s0 += E[o]; n0 += ES[o]; }
-        if (x + 1 < cols) { s1 += E[o + 1]; n1 += ES[o + 1]; }
-        if (x + 2 < cols) { s2 += E[o + 2]; n2 += ES[o + 2]; }
+#pragma unroll
+        for (int q = 0; q < CPL - 1; ++q)
+          if (x + q < cols) { Sa[q] += E[o + q]; Na[q] += ES[o + q]; }
       }
     }
   }
   float* out = scores + slot * score_ld + (col0 - score_col0) + x;
-  const float S[4] = {s0, s1, s2, s3}, N[4] = {n0, n1, n2, n3};
   int nan = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < CPL; ++q) {
     if (x + q < cols) {
       float logit = 0.f;   // empty history: logit 0
-      if (hl > 0) logit = N[q] / ((beta == 0.5f) ? sqrtf(S[q]) : powf(S[q], beta));
+      if (hl > 0) logit = Na[q] / ((beta == 0.5f) ? sqrtf(Sa[q]) : powf(Sa[q], beta));
       float sc = 1.0f / (1.0f + expf(-logit));
       if (logit != logit) {
         sc = __builtin_nanf("");

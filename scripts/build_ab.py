@@ -1,0 +1,14 @@
+"""Build A/B variants of libnais_hip.so with extra -D flags into build_ab/<name>.so (CPU side;
+the .so files travel to the GPU box). Usage: python scripts/build_ab.py name=-DFOO=1,-DBAR=2 ..."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from poi_recommendation_models_amd import build as b  # noqa: E402
+
+out_dir = os.path.join(b.ROOT, "build_ab")
+os.makedirs(out_dir, exist_ok=True)
+for spec in sys.argv[1:]:
+    name, _, flags = spec.partition("=")
+    extra = [f for f in flags.split(",") if f]
+    print(b.build(extra=extra, out=os.path.join(out_dir, name + ".so")), extra, flush=True)
