@@ -26,6 +26,9 @@
 
 namespace {
 
+#ifndef NAIS_GATHER_NT_STORE
+#define NAIS_GATHER_NT_STORE 0   // 1: non-temporal score stores (A/B: keep the stripe in the Infinity Cache)
+#endif
 #ifndef NAIS_GATHER_CPL
 #define NAIS_GATHER_CPL 4   // columns per lane: stripe = 64 * CPL columns (A/B knob)
 #endif
@@ -189,7 +192,8 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
         sc = __builtin_nanf("");
         ++nan;
       }
-      out[q] = sc;
+      if (NAIS_GATHER_NT_STORE) __builtin_nontemporal_store(sc, out + q);
+      else out[q] = sc;
     }
   }
   __threadfence_block();   // this wave's score stores land before its -1 stores below

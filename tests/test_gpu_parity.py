@@ -506,3 +506,33 @@ def test_pairs_auto_choice_and_new4():
     for r, u in enumerate(few):
         assert_topk_equivalent(ia[u].cpu().numpy(), sa[u].cpu().numpy(), ib[r].cpu().numpy(),
                                sb[r].cpu().numpy(), tie_eps=GPU_TIE_EPS)
+
+
+@pytest.mark.parametrize("knobs", [
+    {"PAIR_BLOCK_COLS": 256},                                   # many blocks, overlapped
+    {"PAIR_BLOCK_COLS": 768, "PAIR_FIRST_TABLE_ALL_CUS": False},
+    {"PAIR_TABLE_CUS": 0},                                      # serial, one stream
+    {"PAIR_MEMORY_FRACTION": 2e-6},                             # user passes + minimum block width
+])
+def test_pairs_blocks_passes_bit_identical(knobs):
+    """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, user
+    passes under a small memory budget) never changes a score: top-k ids and scores bit-identical
+    to the default schedule."""
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P, D, H, U, k = 2900, 64, 64, 48, 50
+    data = make_checkins(U, P, 80, seed=41)
+    p = init_nais_params(P, D, H, seed=6, emb_std=0.3, bias_std=0.1)
+    m = _model("basic", p, precision="fp16x3")
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+    ref_ids, ref_sc = _score_topk_pairs(m, csr, range(U), k, None, None, None, None, force=True)
+    saved = {n: getattr(catalog, n) for n in knobs}
+    try:
+        for n, v in knobs.items():
+            setattr(catalog, n, v)
+        ids, sc = _score_topk_pairs(m, csr, range(U), k, None, None, None, None, force=True)
+    finally:
+        for n, v in saved.items():
+            setattr(catalog, n, v)
+    assert torch.equal(ids, ref_ids) and torch.equal(sc, ref_sc)
