@@ -337,6 +337,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         catalog.PAIR_CU_LAYOUT = os.environ["NAIS_PAIR_CU_LAYOUT"]
     if os.environ.get("NAIS_PAIR_BLOCK_COLS"):
         catalog.PAIR_BLOCK_COLS = int(os.environ["NAIS_PAIR_BLOCK_COLS"])
+    for knob in ("PAIR_FUSED_TOPK", "PAIR_LPT_ORDER"):
+        if os.environ.get("NAIS_" + knob):
+            setattr(catalog, knob, os.environ["NAIS_" + knob] == "1")
     if os.environ.get("NAIS_PAIR_FIRST_TABLE_ALL_CUS"):
         catalog.PAIR_FIRST_TABLE_ALL_CUS = os.environ["NAIS_PAIR_FIRST_TABLE_ALL_CUS"] == "1"
     # NAIS_EMULATE_WORLD=N (one process): time rank 0's column shard of an N-GPU run (its tables,
@@ -445,6 +448,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "table_cus": catalog.PAIR_TABLE_CUS, "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
                 "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
+                "fused_topk": catalog.PAIR_FUSED_TOPK, "lpt_order": catalog.PAIR_LPT_ORDER,
                 **({"emulated_world_shard": emulate} if emulate > 1 and world == 1 else {}),
                 "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,
                 "pairs_per_step": pairs_job, "history_entries": entries, "distinct_history_pois": J,

@@ -213,6 +213,14 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *                      scores, 0 for full rows); NaNs counted into *nan_count as
  *                      nais_score_catalog does.
  * The caller loops over column blocks sized to its memory budget and runs nais_topk_rows.
+ *   nais_pair_gather_topk  the same sums and scores, but instead of score rows each user keeps a
+ *                      running top-k: keys[slot*k ..] (uint64, sorted descending, kcount[slot]
+ *                      valid; zero kcount before the first call) with key = ordered(score) << 32 |
+ *                      (0xFFFFFFFF - poi), i.e. torch.topk's (score desc) with ties by POI id asc
+ *                      and NaN first; history POIs are never candidates. Columns of one call may
+ *                      be any block; the calls of one user list must be stream-ordered. k <= 256.
+ *   nais_topk_keys_finish  keys -> out_ids / out_scores [num_users, k] (short lists padded with
+ *                      -1 / NaN and counted into *short_count), as nais_topk_rows reports them.
  */
 size_t nais_pair_rows_workspace_size(int64_t num_pois);
 int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int32_t* users,
@@ -226,6 +234,12 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
                          const int64_t* indptr, const int64_t* indices, const int32_t* users,
                          int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
                          int64_t score_ld, int64_t score_col0, int32_t* nan_count, void* stream);
+int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
+                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, void* stream);
+int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,
+                              int32_t* out_ids, float* out_scores, int32_t* short_count, void* stream);
 
 /*
  * A stream restricted to the CUs whose bits are set in cu_mask[mask_words] (bit i = CU i), for

@@ -27,7 +27,7 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
            "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
            "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
-           "nais_train_backward_ex")
+           "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -190,6 +190,11 @@ def load(path: str | None = None):
     lib.nais_pair_gather.restype = i32
     lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, i64, vp,
                                      vp]
+    lib.nais_pair_gather_topk.restype = i32
+    lib.nais_pair_gather_topk.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp,
+                                          vp]
+    lib.nais_topk_keys_finish.restype = i32
+    lib.nais_topk_keys_finish.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32
     lib.nais_stream_create_cu_mask.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
     lib.nais_stream_destroy.restype = i32

@@ -206,6 +206,11 @@ PAIR_BLOCK_COLS = 1024
 # every CU).
 PAIR_TABLE_CUS = -1
 PAIR_FIRST_TABLE_ALL_CUS = True   # block 0's table (nothing to overlap it with) on every CU
+# Fused gather + running top-k (nais_pair_gather_topk): each user keeps its best k keys while the
+# stripes stream by, so no [users, P] score rows are formed and no top-k pass reads them back
+# (k <= 256, models without a post-gather score fixup).
+PAIR_FUSED_TOPK = True
+PAIR_LPT_ORDER = True   # users launched in decreasing history length
 PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 _masked: dict = {}
 
@@ -276,7 +281,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     lib = _capi.load()
     st = stream if stream is not None else _capi.stream_handle(dev)
     torch_stream = torch.cuda.current_stream(dev)
-    u_all = torch.from_numpy(users.astype(np.int32)).to(dev)
+    # longest histories first: a gather launch then ends on its shortest users (short tail)
+    order = None
+    if PAIR_LPT_ORDER and not rows_only and n > 1:
+        order = np.argsort(-csr.hist_len[users], kind="stable")
+    u_all = torch.from_numpy((users if order is None else users[order]).astype(np.int32)).to(dev)
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
     prm = model.nais_params()
     rowmap = torch.empty(P, dtype=torch.int32, device=dev)
@@ -305,8 +314,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         return None
     free = torch.cuda.mem_get_info(dev)[0]
     budget = int(free * PAIR_MEMORY_FRACTION)
-    # users per pass: their score rows take at most half the budget
-    per_pass = n if rows_only else max(1, min(n, (budget // 2) // (4 * NC)))
+    from .model import _NAISDevice
+    fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256
+             and type(model)._pair_fixup is _NAISDevice._pair_fixup)
+    # users per pass: their score rows take at most half the budget (fused: no score rows)
+    per_pass = n if (rows_only or fused) else max(1, min(n, (budget // 2) // (4 * NC)))
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
     sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -315,7 +327,24 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
-        scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
+        if fused:
+            keys = torch.empty(m, k, dtype=torch.int64, device=dev)
+            kcount = torch.zeros(m, dtype=torch.int32, device=dev)
+
+            def gather(tab, c0, w, stream_):
+                _capi.check(lib.nais_pair_gather_topk(
+                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta), k,
+                    keys.data_ptr(), kcount.data_ptr(), counters[0:1].data_ptr(), stream_),
+                    "nais_pair_gather_topk")
+        else:
+            scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
+
+            def gather(tab, c0, w, stream_):
+                _capi.check(lib.nais_pair_gather(
+                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
+                    scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), stream_), "nais_pair_gather")
         if J > 0:
             W = min(PAIR_BLOCK_COLS, (budget // 4) // (8 * J))
             W = int(min(NC, max(256, W // 256 * 256)))
@@ -353,11 +382,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                             events.append(("table", e_t0, e_t1))
                     e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e_g0.record(gs)
-                    _capi.check(lib.nais_pair_gather(
-                        tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
-                        csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
-                        scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), gs.cuda_stream),
-                        "nais_pair_gather")
+                    gather(tab, c0, w, gs.cuda_stream)
                     e_g1.record(gs)
                     done_g[b % 2] = e_g1
                     if events is not None:
@@ -365,10 +390,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     continue
                 timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
                                                          tab[0].data_ptr(), tab[1].data_ptr(), W, st))
-                timed("gather", lambda: _capi.check(lib.nais_pair_gather(
-                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
-                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
-                    scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), st), "nais_pair_gather"))
+                timed("gather", lambda: gather(tab, c0, w, st))
             if overlap:
                 torch_stream.wait_stream(gs)
                 torch_stream.wait_stream(ts)
@@ -376,20 +398,30 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     t.record_stream(ts)
                     t.record_stream(gs)
             del tabs
-            model._pair_fixup(csr, u_dev, m, scores, c0_all, c1_all, st)
+            if not fused:
+                model._pair_fixup(csr, u_dev, m, scores, c0_all, c1_all, st)
         else:
             scores.fill_(0.5)   # every listed user has an empty history: logit 0 (model.py:79-88)
         if rows_only:
             model._last_nan = counters[0:1]
             return scores
+        if fused:
+            timed("topk", lambda: _capi.check(lib.nais_topk_keys_finish(
+                keys.data_ptr(), kcount.data_ptr(), m, k, ids_out[b0:b0 + m].data_ptr(),
+                sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(), st), "nais_topk_keys_finish"))
+            del keys, kcount
+            continue
         timed("topk", lambda: _capi.check(lib.nais_topk_rows(
             scores.data_ptr(), NC, NC, m, k, ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(),
             counters[1:2].data_ptr(), st), "nais_topk_rows"))
         del scores
     model._last_nan = counters[0:1]
     ids = ids_out.to(torch.int64)
-    if c0_all:
+    if c0_all and not fused:        # the fused keys carry global POI ids already
         ids = torch.where(ids >= 0, ids + c0_all, ids)
+    if order is not None:           # back to the caller's user order
+        inv = torch.from_numpy(np.argsort(order, kind="stable")).to(dev)
+        ids, sc_out = ids.index_select(0, inv), sc_out.index_select(0, inv)
     return ids, sc_out
 
 

@@ -213,6 +213,175 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused gather + running top-k (validation.py:26-27 without the [users, P] score rows).
+// Same sums and score arithmetic as pair_gather_kernel, one launch per 256-column stripe (so the
+// user's list below has one writer per launch). Each user keeps its best k keys so far,
+//   key = ordered(score) << 32 | (0xFFFFFFFF - poi)     (unique: (score desc, id asc), NaN first)
+// sorted descending in keys[slot * k ...] with kcount[slot] of them valid. A wave offers its
+// stripe's candidates (history POIs excluded) that beat the current k-th key; if any do, it merges
+// them with the list in LDS (bitonic, <= k + 256 keys) and writes the new list back. After the
+// first few stripes almost no candidate beats the k-th key, so most waves write nothing.
+constexpr int TK_LDS = 512;                 // keys per wave in LDS: k + 256 <= 512  (k <= 256)
+
+__device__ __forceinline__ uint32_t ord_f32_p(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f32_p(uint32_t o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(GW * 64)
+pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ ES, int64_t ld,
+                        const int32_t* __restrict__ rowmap, const int64_t* __restrict__ indptr,
+                        const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                        int32_t nusers, int64_t col0, int64_t cols, float beta, int k,
+                        unsigned long long* __restrict__ keys, int32_t* __restrict__ kcount,
+                        int32_t* __restrict__ nan_count) {
+  __shared__ unsigned long long lk[GW][TK_LDS];
+  __shared__ uint32_t hm[GW][STRIPE / 32];   // history POIs of this stripe, one bit per column
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t slot = int64_t(blockIdx.x) * GW + w;
+  if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
+  const int64_t u = users[slot];
+  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  const int64_t x = int64_t(lane) * CPL;     // column within the stripe [col0, col0 + cols)
+  const bool full = x + CPL <= cols;
+  if (lane < STRIPE / 32) hm[w][lane] = 0u;
+  wave_lds_sync();
+  float Sa[CPL], Na[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) Sa[q] = Na[q] = 0.f;
+  for (int64_t j0 = 0; j0 < hl; j0 += 64) {
+    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    int64_t mine = 0;
+    if (lane < jn) {
+      const int64_t c = indices[hb + j0 + lane];
+      mine = int64_t(rowmap[c]) * ld;
+      const int64_t r = c - col0;
+      if (r >= 0 && r < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
+    }
+    const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
+    if (full) {
+#pragma unroll 8
+      for (int jj = 0; jj < jn; ++jj) {
+        const int64_t o = bcast64(mlo, mhi, jj) + x;
+        const nfv e = loadv(E + o);
+        const nfv t = loadv(ES + o);
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) {
+          Sa[q] += e[q];
+          Na[q] += t[q];
+        }
+      }
+    } else {
+      for (int jj = 0; jj < jn; ++jj) {
+        const int64_t o = bcast64(mlo, mhi, jj) + x;
+#pragma unroll
+        for (int q = 0; q < CPL - 1; ++q)
+          if (x + q < cols) { Sa[q] += E[o + q]; Na[q] += ES[o + q]; }
+      }
+    }
+  }
+  wave_lds_sync();
+  // the wave's candidates and the current k-th key
+  const int cnt = kcount[slot];
+  const unsigned long long thr = cnt == k ? keys[slot * k + k - 1] : 0ull;   // valid keys are > 0
+  unsigned long long kq[CPL];
+  uint32_t offer = 0;   // bit q: column x + q is offered
+  int nan = 0;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    kq[q] = 0ull;
+    const int64_t r = x + q;
+    if (r < cols && !((hm[w][r >> 5] >> (r & 31)) & 1u)) {
+      float logit = 0.f;   // empty history: logit 0
+      if (hl > 0) logit = Na[q] / ((beta == 0.5f) ? sqrtf(Sa[q]) : powf(Sa[q], beta));
+      float sc = 1.0f / (1.0f + expf(-logit));
+      if (logit != logit) {
+        sc = __builtin_nanf("");
+        ++nan;
+      }
+      kq[q] = ((unsigned long long)ord_f32_p(sc) << 32) |
+              (unsigned long long)(0xFFFFFFFFu - (uint32_t)(col0 + r));
+      if (kq[q] > thr) offer |= 1u << q;
+    }
+  }
+  if (nan_count) {
+    for (int o = 32; o > 0; o >>= 1) nan += __shfl_xor(nan, o);
+    if (lane == 0 && nan) atomicAdd(nan_count, nan);
+  }
+  const int mine_n = __popc(offer);
+  int excl = mine_n;   // inclusive scan over lanes, then exclusive
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(excl, o);
+    if (lane >= o) excl += y;
+  }
+  const int m = __shfl(excl, 63);
+  excl -= mine_n;
+  if (m == 0) return;
+  unsigned long long* L = lk[w];
+  for (int i = lane; i < cnt; i += 64) L[i] = keys[slot * k + i];
+  int pos = cnt + excl;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q)
+    if ((offer >> q) & 1u) L[pos++] = kq[q];
+  const int n = cnt + m;
+  int n2 = 64;
+  while (n2 < n) n2 <<= 1;
+  for (int i = n + lane; i < n2; i += 64) L[i] = 0ull;
+  wave_lds_sync();
+  // bitonic sort, descending
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < n2; i += 64) {
+        const int partner = i ^ stride;
+        if (partner > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long a = L[i], b = L[partner];
+          if (desc ? (a < b) : (a > b)) {
+            L[i] = b;
+            L[partner] = a;
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  const int nk = n < k ? n : k;
+  for (int i = lane; i < nk; i += 64) keys[slot * k + i] = L[i];
+  if (lane == 0) kcount[slot] = nk;
+}
+
+// keys -> (ids, scores) of the top-k lists; short lists padded with -1 / NaN and counted
+__global__ void topk_keys_finish_kernel(const unsigned long long* __restrict__ keys,
+                                        const int32_t* __restrict__ kcount, int32_t n, int k,
+                                        int32_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                                        int32_t* __restrict__ short_count) {
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= int64_t(n) * k) return;
+  const int64_t slot = i / k;
+  const int r = int(i % k);
+  const int cnt = kcount[slot];
+  int32_t id = -1;
+  float sc = __builtin_nanf("");
+  if (r < cnt) {
+    const unsigned long long key = keys[i];
+    id = (int32_t)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+    sc = unord_f32_p((uint32_t)(key >> 32));
+  }
+  out_ids[i] = id;
+  out_scores[i] = sc;
+  if (r == 0 && cnt < k && short_count) atomicAdd(short_count, 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -265,6 +434,43 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
                      dim3(GW * 64), 0, st, e, es, ld, rowmap, indptr, indices, users, num_users, col0,
                      cols, beta, scores, score_ld, score_col0, nan_count);
   return nais_internal_check_launch("pair_gather_kernel");
+}
+
+int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
+                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || k <= 0)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (k > TK_LDS - STRIPE) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
+  if (col0 + cols > 0xFFFFFFFFll) return nais_internal_fail(NAIS_E_UNSUPPORTED, "POI ids must fit 32 bits");
+  if (num_users == 0 || cols == 0) return NAIS_OK;
+  if (!e || !es || !rowmap || !indptr || !indices || !users || !keys || !kcount)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  if (ld % 4 != 0) return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned groups = (unsigned)((num_users + GW - 1) / GW);
+  for (int64_t s0 = 0; s0 < cols; s0 += STRIPE) {   // one launch per stripe: one writer per list
+    hipLaunchKernelGGL(pair_gather_topk_kernel, dim3(groups), dim3(GW * 64), 0, st, e + s0, es + s0, ld,
+                       rowmap, indptr, indices, users, num_users, col0 + s0,
+                       std::min<int64_t>(STRIPE, cols - s0), beta, (int)k,
+                       reinterpret_cast<unsigned long long*>(keys), kcount, nan_count);
+    const int32_t rc = nais_internal_check_launch("pair_gather_topk_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,
+                              int32_t* out_ids, float* out_scores, int32_t* short_count, void* stream) {
+  if (num_users < 0 || k <= 0) return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (num_users == 0) return NAIS_OK;
+  if (!keys || !kcount || !out_ids || !out_scores) return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  const int64_t total = int64_t(num_users) * k;
+  hipLaunchKernelGGL(topk_keys_finish_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const unsigned long long*>(keys),
+                     kcount, num_users, (int)k, out_ids, out_scores, short_count);
+  return nais_internal_check_launch("topk_keys_finish_kernel");
 }
 
 int32_t nais_stream_create_cu_mask(const uint32_t* cu_mask, uint32_t mask_words, void** stream) {

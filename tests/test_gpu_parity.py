@@ -512,12 +512,16 @@ def test_pairs_auto_choice_and_new4():
     {"PAIR_BLOCK_COLS": 256},                                   # many blocks, overlapped
     {"PAIR_BLOCK_COLS": 768, "PAIR_FIRST_TABLE_ALL_CUS": False},
     {"PAIR_TABLE_CUS": 0},                                      # serial, one stream
-    {"PAIR_MEMORY_FRACTION": 2e-6},                             # user passes + minimum block width
+    {"PAIR_MEMORY_FRACTION": 2e-6},                             # minimum block width
+    {"PAIR_FUSED_TOPK": False},                                 # score rows + nais_topk_rows
+    {"PAIR_FUSED_TOPK": False, "PAIR_MEMORY_FRACTION": 2e-6},   # ... in user passes
+    {"PAIR_LPT_ORDER": False},                                  # users in the caller's order
+    {"PAIR_LPT_ORDER": False, "PAIR_FUSED_TOPK": False},
 ])
 def test_pairs_blocks_passes_bit_identical(knobs):
-    """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, user
-    passes under a small memory budget) never changes a score: top-k ids and scores bit-identical
-    to the default schedule."""
+    """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, the
+    fused running top-k or score rows + a top-k pass, user passes under a small memory budget)
+    never changes a result: top-k ids and scores bit-identical to the default schedule."""
     from poi_recommendation_models_amd import catalog
     from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
