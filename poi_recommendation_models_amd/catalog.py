@@ -195,8 +195,11 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
 # 100000. Overlapped (below; profiles/r1/overlap/): 1024 / 2048 / 3072 / 4096 / 8192 columns ->
 # 606 / 610 / 619 / 627 / 665 ms per config-4 step (a shorter pipeline fill). With block 0's table
 # on every CU (profiles/r1/blocks/): 1024 vs 2048 -> 579.8 vs 581.3 ms at N = 1, and on one rank's
-# column shard of an 8-GPU run (12.5k columns) 512 / 1024 / 2048 -> 77.2 / 77.7 / 79.9 ms.
-PAIR_BLOCK_COLS = 1024
+# column shard of an 8-GPU run (12.5k columns) 512 / 1024 / 2048 -> 77.2 / 77.7 / 79.9 ms. With the
+# fused top-k, longest-first users and no host syncs (profiles/r1/blocks2/): 256 / 512 / 1024 ->
+# 545.9 / 546.0 / 548.0 ms at N = 1 and 71.5 / 72.3 / 73.3 ms on the 8-GPU shard, where 256 brings
+# the tables (65.8 ms on half the CUs) close to the gathers (67.7 ms): 512 keeps a margin.
+PAIR_BLOCK_COLS = 512
 # Table (MFMA-bound) and gather (HBM-bound) phases of consecutive column blocks run side by side
 # on CU-masked streams: tables on CUs [0, PAIR_TABLE_CUS), gathers on the rest (-1 = half the
 # device's CUs, i.e. 4 of the 8 XCDs each; 0 = serial on the caller's stream). Double-buffered
@@ -285,7 +288,12 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     order = None
     if PAIR_LPT_ORDER and not rows_only and n > 1:
         order = np.argsort(-csr.hist_len[users], kind="stable")
-    u_all = torch.from_numpy((users if order is None else users[order]).astype(np.int32)).to(dev)
+    # one pinned, non-blocking upload of the launch order (and its inverse): no host sync here or
+    # at the end of the job, which would idle the GPU between consecutive jobs
+    up = np.concatenate([users if order is None else users[order],
+                         np.argsort(order, kind="stable") if order is not None else np.zeros(0, np.int64)])
+    up_dev = torch.from_numpy(up.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
+    u_all = up_dev[:n]
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
     prm = model.nais_params()
     rowmap = torch.empty(P, dtype=torch.int32, device=dev)
@@ -420,7 +428,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if c0_all and not fused:        # the fused keys carry global POI ids already
         ids = torch.where(ids >= 0, ids + c0_all, ids)
     if order is not None:           # back to the caller's user order
-        inv = torch.from_numpy(np.argsort(order, kind="stable")).to(dev)
+        inv = up_dev[n:]
         ids, sc_out = ids.index_select(0, inv), sc_out.index_select(0, inv)
     return ids, sc_out
 
