@@ -375,10 +375,12 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        per = {}
+        per, nl = {}, {}
         for step_ev in evs:
-            for kind, e0, e1 in step_ev:
+            for kind, e0, e1, launches in step_ev:
                 per.setdefault(kind, []).append(e0.elapsed_time(e1))
+                nl[kind] = nl.get(kind, 0) + launches
+        per["_launches"] = nl
         return el, per
 
     elapsed, per = run(a.precision, a.warmup, a.steps)
@@ -396,7 +398,12 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     entries = int(hist_len.sum())
     J = int(np.count_nonzero(np.bincount(data.indices, minlength=P)))
     # algorithmic work per step on this rank
-    gather_bytes = entries * NC * 8 + a.num_users * NC * 4 + entries * 12   # table rows, scores, ids
+    fused = catalog.PAIR_FUSED_TOPK and K <= 256
+    Wb, st_w = catalog.PAIR_BLOCK_COLS, catalog.PAIR_STRIPE
+    stripes = sum((min(Wb, NC - b) + st_w - 1) // st_w for b in range(0, NC, Wb))
+    # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B per
+    # entry) + score rows (4 B per user x column; the fused kernel writes only the top-k merges)
+    gather_bytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     table_flops = J * NC * flop_per_pair_item
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -404,11 +411,11 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     g_ms = sum(per.get("gather", [])) / a.steps
     t_ms = sum(per.get("table", [])) / a.steps
     k_ms = sum(per.get("topk", [])) / a.steps
-    n_gl = max(1, len(per.get("gather", [])) // a.steps)
+    n_gl = max(1, per["_launches"].get("gather", 0) // a.steps)
     achieved = gather_bytes / (g_ms * 1e-3) / 1e9
     traffic = None
     try:
-        tj = json.load(open(a.traffic_json)).get("pairs_gather", {})
+        tj = json.load(open(a.traffic_json)).get("pairs_gather_topk" if fused else "pairs_gather", {})
         if (tj.get("num_users") == a.num_users and tj.get("num_pois") == P and tj.get("world") == world
                 and tj.get("block_cols") == catalog.PAIR_BLOCK_COLS):
             traffic = tj.get("hbm_bytes_per_launch")
@@ -456,7 +463,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                                "tables replicated, one all-gather + merge of the top-k blocks",
             },
             "roofline": {
-                "kernel": "pair_gather_kernel (nais_pair_gather)",
+                "kernel": "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
+                          "pair_gather_kernel (nais_pair_gather)",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": 8000.0,
@@ -466,9 +474,11 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "algorithmic_bytes_per_launch": gather_bytes / n_gl,
                 "avg_launch_ms": g_ms / n_gl,
                 "launches_per_step": n_gl,
-                "note": "algorithmic bytes = sum_u h_u x columns x 8 B table reads + score writes; the "
-                        "stripe order lets the Infinity Cache serve part of the reads, so HBM traffic "
-                        "(see traffic) can be below them",
+                "note": "algorithmic bytes per launch (one 256-column stripe for the fused kernel) = "
+                        "sum_u h_u x columns x 8 B table reads + 12 B CSR id + row map per history "
+                        "entry (+ 4 B score writes per user x column, non-fused); traffic = "
+                        "rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per launch, Infinity-Cache hits "
+                        "included",
                 "overlap": "tables on CUs [0, %d) and gathers on the other %d, side by side on "
                            "CU-masked streams (double-buffered tables)" % (table_cus, ncu - table_cus)
                            if table_cus < ncu else "serial",

@@ -214,6 +214,7 @@ PAIR_FIRST_TABLE_ALL_CUS = True   # block 0's table (nothing to overlap it with)
 # (k <= 256, models without a post-gather score fixup).
 PAIR_FUSED_TOPK = True
 PAIR_LPT_ORDER = True   # users launched in decreasing history length
+PAIR_STRIPE = 256       # columns per gather wave (nais_pairs.hip STRIPE)
 PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 _masked: dict = {}
 
@@ -301,14 +302,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     ws = _workspace(dev, lib.nais_pair_rows_workspace_size(P))
 
-    def timed(kind, fn):
+    def timed(kind, fn, launches=1):
         if events is None:
             return fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(torch_stream)
         r = fn()
         e1.record(torch_stream)
-        events.append((kind, e0, e1))
+        events.append((kind, e0, e1, launches))
         return r
 
     def rows(u_dev, m):
@@ -335,6 +336,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
+        def gather_launches(w):   # nais_pair_gather_topk launches one kernel per 256-column stripe
+            return (w + PAIR_STRIPE - 1) // PAIR_STRIPE if fused else 1
         if fused:
             keys = torch.empty(m, k, dtype=torch.int64, device=dev)
             kcount = torch.zeros(m, dtype=torch.int32, device=dev)
@@ -387,18 +390,18 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         e_t1.record(ts)
                         gs.wait_event(e_t1)
                         if events is not None:
-                            events.append(("table", e_t0, e_t1))
+                            events.append(("table", e_t0, e_t1, 1))
                     e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e_g0.record(gs)
                     gather(tab, c0, w, gs.cuda_stream)
                     e_g1.record(gs)
                     done_g[b % 2] = e_g1
                     if events is not None:
-                        events.append(("gather", e_g0, e_g1))
+                        events.append(("gather", e_g0, e_g1, gather_launches(w)))
                     continue
                 timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
                                                          tab[0].data_ptr(), tab[1].data_ptr(), W, st))
-                timed("gather", lambda: gather(tab, c0, w, st))
+                timed("gather", lambda: gather(tab, c0, w, st), gather_launches(w))
             if overlap:
                 torch_stream.wait_stream(gs)
                 torch_stream.wait_stream(ts)

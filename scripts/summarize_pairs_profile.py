@@ -16,7 +16,7 @@ rows = []
 for sub in ("pmc_fetch", "pmc_write"):
     for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
         n = r["Kernel_Name"]
-        if any(t in n for t in ("pair_gather", "catalog", "topk")):
+        if any(t in n for t in ("pair_gather", "catalog", "topk")):  # noqa: E501
             name = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             rows.append({"kernel": name, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
                          "value_kb": float(r["Counter_Value"]), "grid": r["Grid_Size"],
@@ -26,7 +26,8 @@ with open(os.path.join(dst, "pmc_summary.csv"), "w", newline="") as fh:
     w.writeheader()
     w.writerows(rows)
 out = {}
-for tag, key in (("pair_gather", "pairs_gather"), ("catalog", "pairs_table")):
+for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
+                 ("catalog", "pairs_table")):
     sel = [r for r in rows if tag in r["kernel"]]
     f = [r["value_kb"] for r in sel if r["counter"] == "FETCH_SIZE"]
     wr = [r["value_kb"] for r in sel if r["counter"] == "WRITE_SIZE"]
