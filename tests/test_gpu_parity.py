@@ -540,3 +540,39 @@ def test_pairs_blocks_passes_bit_identical(knobs):
         for n, v in saved.items():
             setattr(catalog, n, v)
     assert torch.equal(ids, ref_ids) and torch.equal(sc, ref_sc)
+
+
+@pytest.mark.parametrize("k", [1, 50, 256, 300])
+@pytest.mark.parametrize("variant", ["basic", "region", "region_distance", "distance"])
+def test_pairs_fused_topk_equals_score_rows(variant, k):
+    """The fused running top-k (k <= 256) and the score-row route (k > 256 falls back to it) give
+    the same ids and scores for every variant, including NaN scores (a NaN history embedding makes
+    a user's whole row NaN, ranked first like torch.topk, ties by id)."""
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P, D, H, U = 1500, 32, 32, 24
+    data = make_checkins(U, P, 40, seed=17, num_regions=16)
+    p = init_nais_params(P, D, H, seed=9, emb_std=0.3, variant=variant, num_regions=16, bias_std=0.1)
+    hot = int(data.indices[data.indptr[2]])            # user 2's first history POI
+    p["embed_history.weight"][hot] = np.nan            # NaN through h . t: user 2's rows are NaN
+    m = _model(variant, p, precision="fp16x3")
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+    kw = {} if variant in ("basic", "distance") else {"region_of": data.region_of}
+    if "distance" in variant:
+        kw["coords"] = data.place_coords
+    args = (kw.get("region_of"), kw.get("coords"), None, None)
+    saved = catalog.PAIR_FUSED_TOPK
+    try:
+        catalog.PAIR_FUSED_TOPK = False
+        ref_ids, ref_sc = _score_topk_pairs(m, csr, range(U), k, *args, force=True)
+        catalog.PAIR_FUSED_TOPK = True
+        ids, sc = _score_topk_pairs(m, csr, range(U), k, *args, force=True)
+    finally:
+        catalog.PAIR_FUSED_TOPK = saved
+    assert torch.equal(ids, ref_ids)
+    a, b = sc.cpu().numpy(), ref_sc.cpu().numpy()
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    np.testing.assert_array_equal(a[~np.isnan(a)], b[~np.isnan(b)])
+    if variant == "basic" and k == 50:
+        assert np.isnan(a).any()                        # the NaN rows were exercised
