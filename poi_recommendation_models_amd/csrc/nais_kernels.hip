@@ -557,6 +557,13 @@ __device__ __forceinline__ void split8(const float (&x)[8], half8& hi, half8& lo
   lo = *reinterpret_cast<const half8*>(&lu);
 }
 
+// Both lane halves' values of v in every lane, by one v_permlane32_swap (VALU, no LDS):
+// .x = v[lane & 31], .y = v[32 + (lane & 31)]; .x + .y == v + shfl_xor(v, 32) exactly.
+__device__ __forceinline__ float2 lane_halves(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ float block_max(float v, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -888,6 +895,12 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   using C = CfgB<DH, HB, DIST>;
   constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
   constexpr bool EREGS = HB <= 2 && DH <= 32;
+  // s = h_j . t_c for the chunk's 32 items on the matrix pipe (one 32x32 tile per wave and chunk,
+  // the same split-fp16 3-product scheme) instead of a 2*DH-term VALU dot per item and lane
+#ifndef NAIS_X3B_SMFMA
+#define NAIS_X3B_SMFMA 1
+#endif
+  constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][hi|lo][NE]
   float* Adist = reinterpret_cast<float*>(ring + 2 * G * 2 * NE);
@@ -1019,6 +1032,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 
   float Sacc = 1.f, invS = 1.f;
   int64_t j0 = 0;   // history chunk base (the step's table-mode write needs it)
+  floatx16 sacc;                 // SMF: s tile [32 chunk items x 32 candidates], scaled by Sh*St
+  float invShSt = 1.f;
 
   // One pipeline step: the MFMA chain of item `cur` (A_j from the ring slot `src`, t_c from VGPRs)
   // into accN, with the VALU epilogue of the previous item (accP, chunk-local `prev`) cut into KS
@@ -1057,13 +1072,15 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
       for (int v = s * VPS; v < (s + 1) * VPS && v < NV; ++v)
         ap += epi.term(v, accP[v / 16][v % 16], invS);
+      if (!SMF) {
 #pragma unroll
-      for (int q = s * QPS; q < (s + 1) * QPS && q < DH / 4; ++q) {
-        const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * q);
-        sd = __builtin_fmaf(tv[4 * q], hv.x, sd);
-        sd = __builtin_fmaf(tv[4 * q + 1], hv.y, sd);
-        sd = __builtin_fmaf(tv[4 * q + 2], hv.z, sd);
-        sd = __builtin_fmaf(tv[4 * q + 3], hv.w, sd);
+        for (int q = s * QPS; q < (s + 1) * QPS && q < DH / 4; ++q) {
+          const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * q);
+          sd = __builtin_fmaf(tv[4 * q], hv.x, sd);
+          sd = __builtin_fmaf(tv[4 * q + 1], hv.y, sd);
+          sd = __builtin_fmaf(tv[4 * q + 2], hv.z, sd);
+          sd = __builtin_fmaf(tv[4 * q + 3], hv.w, sd);
+        }
       }
       if (NAIS_X3B_SCHED) __builtin_amdgcn_sched_barrier(0);
     }
@@ -1080,8 +1097,16 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
       for (int hb = 0; hb < HB; ++hb) accN[hb] = mfma32(Adist[hb * 64 + lane], fs, accN[hb]);
     }
-    const float a = ap + __shfl_xor(ap, 32);
-    const float sv = (sd + __shfl_xor(sd, 32)) * invSt;
+    const float2 aph = lane_halves(ap);
+    const float a = aph.x + aph.y;
+    float sv;
+    if (SMF) {   // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
+      const float2 sh2 = lane_halves(sacc[((pj >> 3) << 2) | (pj & 3)]);
+      sv = (((pj >> 2) & 1) ? sh2.y : sh2.x) * invShSt;
+    } else {
+      const float2 sdh = lane_halves(sd);
+      sv = (sdh.x + sdh.y) * invSt;
+    }
     const bool keep = hid[pj] != (int32_t)c;
     const float e = expf(a) * (keep ? 1.f : 0.f);
     if (live) {
@@ -1124,8 +1149,33 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         hco[2 * jj + 1] = coords[2 * item + 1];
       }
     }
-    const float SA = pow2_scale(Wmax * block_max(hmax, red));   // barrier: chunk published
+    const float Hm = block_max(hmax, red);                        // barrier: chunk published
+    const float SA = pow2_scale(Wmax * Hm);
     const float rs = SA / SAcur;                                  // exact power-of-two ratio
+    if (SMF) {
+      const float Sh = pow2_scale(Hm);
+      invShSt = 1.f / (Sh * St);
+      const int m = lane & 31;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        float x[8];
+        const float* hp = hrows + m * D + hh * DH + 8 * s;
+        const float4 h0 = *reinterpret_cast<const float4*>(hp);
+        const float4 h1 = *reinterpret_cast<const float4*>(hp + 4);
+        const bool ok = m < jn;
+        x[0] = ok ? h0.x * Sh : 0.f; x[1] = ok ? h0.y * Sh : 0.f;
+        x[2] = ok ? h0.z * Sh : 0.f; x[3] = ok ? h0.w * Sh : 0.f;
+        x[4] = ok ? h1.x * Sh : 0.f; x[5] = ok ? h1.y * Sh : 0.f;
+        x[6] = ok ? h1.z * Sh : 0.f; x[7] = ok ? h1.w * Sh : 0.f;
+        half8 ah, al;
+        split8(x, ah, al);
+        sacc = mfma16(al, tb_hi[s], sacc);
+        sacc = mfma16(ah, tb_lo[s], sacc);
+        sacc = mfma16(ah, tb_hi[s], sacc);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < EPT; ++q)
 #pragma unroll
