@@ -837,11 +837,20 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
       const float sv = (sd + __shfl_xor(sd, 32)) * invSt;
       const bool keep = hid[jj] != (int32_t)c;
       const float e = expf(a) * (keep ? 1.f : 0.f);
+      if (tab.e) {   // pair-table mode: the pair's two terms instead of the user's sums
+        if (valid && hh == 0) {
+          const int64_t o = (hbeg + j0 + jj) * tab.ld + (c - tab.col0);
+          tab_store(tab.e + o, e);
+          tab_store(tab.es + o, e * sv);
+        }
+        continue;
+      }
       in_hist |= !keep;
       S += e;
       N += e * sv;
     }
   }
+  if (tab.e) return;
 
   const float logit = finish_logit(S, N, p.beta, hlen == 0);
   const bool isnan_ = logit != logit;
@@ -1821,10 +1830,10 @@ template <int DH, int HB, int VAR>
 int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                       const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                       const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
-                      hipStream_t stream) {
+                      hipStream_t stream, const TableOut& tab = TableOut{}) {
   if constexpr (DH % 8 != 0) {  // D = 8: one K=16 f16 step would be half padding; use fp32
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
-                                       scores, ld, nan_count, stream);
+                                       scores, ld, nan_count, stream, tab);
   } else {
     const size_t lds = catalog_x3_lds<DH, HB, VAR>();
     auto kern = catalog_score_x3_kernel<DH, HB, VAR>;
@@ -1834,9 +1843,9 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid = cat_grid(d.P, nb, CAND_PER_BLOCK);
+    dim3 grid = tab.e ? table_grid(tab, nb) : cat_grid(d.P, nb, CAND_PER_BLOCK);
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
-                       coords, latlon_mat, scores, ld, nan_count, TableOut{});
+                       coords, latlon_mat, scores, ld, nan_count, tab);
     return check_launch("catalog_score_x3_kernel");
   }
 }
@@ -1850,12 +1859,10 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
   } else if constexpr (!(HB <= 2 && DH <= 32 && !VarT<VAR>::DIST)) {
-    if (tab.e)   // table mode has no per-pair split variant: exact fp32 kernel
-      return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
-                                         latlon_mat, scores, ld, nan_count, stream, tab);
-    // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel
+    // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel (also
+    // in pair-table mode)
     return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
-                                          latlon_mat, scores, ld, nan_count, stream);
+                                          latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
     const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST>::BYTES;
     auto kern = catalog_score_x3b_kernel<DH, HB, VAR>;
