@@ -378,6 +378,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         per, nl = {}, {}
         for step_ev in evs:
             for kind, e0, e1, launches in step_ev:
+                if e0 is None:          # a setting, not a timed launch
+                    per[kind] = launches
+                    continue
                 per.setdefault(kind, []).append(e0.elapsed_time(e1))
                 nl[kind] = nl.get(kind, 0) + launches
         per["_launches"] = nl
@@ -407,7 +410,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     table_flops = J * NC * flop_per_pair_item
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    table_cus = ncu // 2 if catalog.PAIR_TABLE_CUS < 0 else (catalog.PAIR_TABLE_CUS or ncu)
+    table_cus = per.get("table_cus", ncu) or ncu
     g_ms = sum(per.get("gather", [])) / a.steps
     t_ms = sum(per.get("table", [])) / a.steps
     k_ms = sum(per.get("topk", [])) / a.steps
@@ -452,7 +455,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
                             "score + top-%d; one step = every user's whole catalog" % (a.num_users, P, D, K),
                 "model": "NAIS_basic", "strategy": "pairs", "num_users": a.num_users, "num_pois": P,
-                "table_cus": catalog.PAIR_TABLE_CUS, "cu_layout": catalog.PAIR_CU_LAYOUT,
+                "table_cus": table_cus, "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
                 "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
                 "fused_topk": catalog.PAIR_FUSED_TOPK, "lpt_order": catalog.PAIR_LPT_ORDER,

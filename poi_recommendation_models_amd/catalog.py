@@ -219,6 +219,25 @@ PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 _masked: dict = {}
 
 
+def auto_table_cus(model, J, NC, entries, ncu):
+    """CUs for the table stream (the rest gather), in whole XCDs (ncu / 8), from a cost model fitted
+    on config 4 and config 5 (profiles/r1/cfg5p/): tables at ~1.1e15 f16 FLOP/s (split-fp16) or
+    1.3e14 FLOP/s (fp32) on the whole chip, scaling with their CUs; gathers at ~60 GB/s per CU up
+    to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 128 of 256,
+    config 5: 224)."""
+    H, din = model.attn_layer1.weight.shape
+    split = getattr(model, "precision", "fp16x3") != "fp32"
+    t_tab = J * NC * 2.0 * H * din * (3 if split else 1) / (1.1e15 if split else 1.3e14)
+    gbytes = entries * NC * 8.0
+    xcd = max(1, ncu // 8)
+    best, best_t = ncu // 2, None
+    for n in range(ncu // 2, ncu - xcd + 1, xcd):
+        t = max(t_tab * ncu / n, gbytes / min(7.5e12, (ncu - n) * 60e9))
+        if best_t is None or t < best_t:
+            best, best_t = n, t
+    return best
+
+
 def _destroy_masked_streams():
     """Release the CU-masked streams before interpreter exit: left to the C++ static destructors
     they outlive the HIP runtime (a crash at exit under rocprofv3)."""
@@ -361,7 +380,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             W = int(min(NC, max(256, W // 256 * 256)))
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            table_cus = ncu // 2 if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS
+            table_cus = (auto_table_cus(model, J, NC, entries, ncu) if PAIR_TABLE_CUS < 0
+                         else PAIR_TABLE_CUS)
+            if events is not None:
+                events.append(("table_cus", None, None, table_cus))
             overlap = 0 < table_cus < ncu and len(blocks) > 1 and stream is None
             tabs = [torch.empty(2, J, W, dtype=torch.float32, device=dev)
                     for _ in range(2 if overlap else 1)]
