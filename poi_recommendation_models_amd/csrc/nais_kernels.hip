@@ -41,6 +41,13 @@ namespace {
 #ifndef NAIS_X3B_SCHED
 #define NAIS_X3B_SCHED 0
 #endif
+#ifndef NAIS_X3B_WIDE
+// 1: the item-side split kernel also for D or H > 64, as 4 waves with one wave per SIMD (512-VGPR
+// budget). Parity-green but slower at D = H = 128 (config 5: 285 vs 386 TF direct, 237 vs 319 TF
+// tables; profiles/r1/cfg5ab/): the per-item A_j build (8 fragments per thread, W1 values held in
+// AGPRs) cannot hide under another wave's MFMAs. 0 (default): the per-pair split kernel there.
+#define NAIS_X3B_WIDE 0
+#endif
 constexpr int WAVES = NAIS_WAVES;           // 512-thread workgroups
 constexpr int THREADS = WAVES * 64;
 constexpr int CAND_PER_BLOCK = WAVES * 32;  // one 32-candidate MFMA column tile per wave
@@ -97,8 +104,8 @@ struct TableOut {
 // Infinity Cache serves the re-reads at ~40 GB/s, far below any limit.
 __device__ __forceinline__ int cat_user_slot() { return NAIS_TILE_MAJOR ? blockIdx.x : blockIdx.y; }
 __device__ __forceinline__ int cat_tile() { return NAIS_TILE_MAJOR ? blockIdx.y : blockIdx.x; }
-inline dim3 table_grid(const TableOut& t, int ngroups) {
-  return dim3((unsigned)((t.cols + CAND_PER_BLOCK - 1) / CAND_PER_BLOCK), (unsigned)ngroups);
+inline dim3 table_grid(const TableOut& t, int ngroups, int cand_per_block = CAND_PER_BLOCK) {
+  return dim3((unsigned)((t.cols + cand_per_block - 1) / cand_per_block), (unsigned)ngroups);
 }
 inline dim3 cat_grid(int64_t P, int nb, int cand_per_block) {
   const unsigned tiles = (unsigned)((P + cand_per_block - 1) / cand_per_block);
@@ -564,6 +571,20 @@ __device__ __forceinline__ float2 lane_halves(float v) {
   return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+template <int NW>
+__device__ float block_max_n(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float m = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+  return m;
+}
+
 __device__ float block_max(float v, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
@@ -873,7 +894,7 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // candidate into B fragments that stay in VGPRs for the whole sweep. The per-(c, j) VALU work
 // is then only the epilogue and h_j . t_c -- no per-pair conversions.
 // ---------------------------------------------------------------------------------------------
-template <int DH, int HB, bool DIST>
+template <int DH, int HB, bool DIST, int NW = WAVES>
 struct CfgB {
   static constexpr int D = 2 * DH;
   static constexpr int KS = DH / 8;
@@ -885,15 +906,17 @@ struct CfgB {
   static constexpr int G = IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1);   // items per ring group
 #endif
   static constexpr int JCB = (2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;  // LDS chunk rows
-  static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread
+  static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);  // build entries per thread
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
   static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
                                   size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
 };
 
-template <int DH, int HB, int VAR>
-__global__ void __launch_bounds__(THREADS, 1)
+// NW = waves per workgroup: 8 (2 waves per SIMD, <= 256 VGPRs) for D, H <= 64; 4 (one wave per
+// SIMD, up to 512 VGPRs: both pipelined accumulator sets and b1 / w2 stay in registers) above.
+template <int DH, int HB, int VAR, int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
 catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                          const int64_t* __restrict__ region_of, const double* __restrict__ coords,
@@ -901,9 +924,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
   constexpr bool REGION = VarT<VAR>::REGION;
   constexpr bool DIST = VarT<VAR>::DIST;
-  using C = CfgB<DH, HB, DIST>;
+  using C = CfgB<DH, HB, DIST, NW>;
   constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
-  constexpr bool EREGS = HB <= 2 && DH <= 32;
+  constexpr int THREADS = NW * 64, CAND_PER_BLOCK = NW * 32;   // shadow the 8-wave defaults
+  constexpr bool EREGS = (HB <= 2 && DH <= 32) || NW == 4;
   // s = h_j . t_c for the chunk's 32 items on the matrix pipe (one 32x32 tile per wave and chunk,
   // the same split-fp16 3-product scheme) instead of a 2*DH-term VALU dot per item and lane
 #ifndef NAIS_X3B_SMFMA
@@ -947,7 +971,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       wmax = fmaxf(wmax, fabsf(wv[q][x]));
     }
   }
-  const float Wmax = block_max(wmax, red);
+  const float Wmax = block_max_n<NW>(wmax, red);
   if (DIST) {
     for (int f = tid; f < C::ADIST; f += THREADS) {
       const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
@@ -1158,7 +1182,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         hco[2 * jj + 1] = coords[2 * item + 1];
       }
     }
-    const float Hm = block_max(hmax, red);                        // barrier: chunk published
+    const float Hm = block_max_n<NW>(hmax, red);                        // barrier: chunk published
     const float SA = pow2_scale(Wmax * Hm);
     const float rs = SA / SAcur;                                  // exact power-of-two ratio
     if (SMF) {
@@ -1858,22 +1882,23 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
-  } else if constexpr (!(HB <= 2 && DH <= 32 && !VarT<VAR>::DIST)) {
-    // the two pipelined accumulator sets do not fit 256 VGPRs here: per-pair split kernel (also
-    // in pair-table mode)
+  } else if constexpr (VarT<VAR>::DIST || (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32))) {
+    // the distance features ride on the per-pair split kernel (also in pair-table mode)
     return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
                                           latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
-    const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST>::BYTES;
-    auto kern = catalog_score_x3b_kernel<DH, HB, VAR>;
+    // D, H <= 64: 8 waves (2 per SIMD); larger: 4 waves, one per SIMD, 512-VGPR budget
+    constexpr int NW = (HB <= 2 && DH <= 32) ? WAVES : 4;
+    const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW>::BYTES;
+    auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
-    dim3 grid = tab.e ? table_grid(tab, nb) : cat_grid(d.P, nb, CAND_PER_BLOCK);
-    hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
+    dim3 grid = tab.e ? table_grid(tab, nb, NW * 32) : cat_grid(d.P, nb, NW * 32);
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, stream, d, indptr, indices, users, region_of,
                        coords, latlon_mat, scores, ld, nan_count, tab);
     return check_launch("catalog_score_x3b_kernel");
   }
