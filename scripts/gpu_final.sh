@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-end evidence: GPU suite, smoke(), the default bench line, and the rocprofv3 kernel trace +
+# FETCH_SIZE / WRITE_SIZE passes of the same bench command (gpu_profile.sh).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+cut -c1-400 gpurun_out/bench.json
+scripts/gpu_profile.sh "$@"
