@@ -1,19 +1,88 @@
 """Ranking metrics on the host (same names, arguments and results as eval_metrics.py:3-69).
 
-The reference fans each metric out to a `multiprocessing.Pool(len(k_list))` (eval_metrics.py:9-25),
-forking 3 x len(k_list) processes per call; the values are the same when computed in-process,
-which is what `evaluate_mp` does here. Errors match: recall/hit divide by the number of users
-with a non-empty positive list (ZeroDivisionError when there is none, eval_metrics.py:56,69).
+The reference fans each metric out to a `multiprocessing.Pool(len(k_list))` (eval_metrics.py:9-25)
+and loops over users with Python sets. Here one vectorised pass builds the [users, k] hit matrix
+(`np.isin` on (user, POI) codes; positives deduplicated like `set(actual[i])`) and every k of
+every metric is a prefix count of it. The float results are bit-identical to the reference's:
+each per-user term is the same IEEE division, and the terms are summed left to right in user
+order (`np.add.accumulate` is sequential, as the reference's `+=` loop is), then divided once.
+Config 4 (50k users, k_list of 6): ~0.1 s instead of seconds of set intersections.
+Errors match: recall/hit divide by the number of users with a non-empty positive list
+(ZeroDivisionError when there is none, eval_metrics.py:56,69).
 """
 from __future__ import annotations
 
+import numpy as np
+
+
+def _seq_sum(vals):
+    """Python's left-to-right `s = 0.0; s += v` over float64 values."""
+    if len(vals) == 0:
+        return 0.0
+    return float(np.add.accumulate(np.asarray(vals, dtype=np.float64))[-1])
+
+
+class _Hits:
+    """hit[u, r] = predicted[u][r] in set(actual[u]); n_act[u] = len(set(actual[u]))."""
+
+    def __init__(self, actual, predicted):
+        n = len(predicted)
+        rl = [len(p) for p in predicted] if not isinstance(predicted, np.ndarray) else None
+        K = predicted.shape[1] if rl is None else max(rl, default=0)
+        if rl is None or all(r == K for r in rl):
+            pred = np.asarray(predicted, dtype=np.int64).reshape(n, K)
+        else:                                   # ragged lists: pad with -1, which never hits
+            pred = np.full((n, K), -1, np.int64)
+            for i, p in enumerate(predicted):
+                pred[i, :len(p)] = p
+        lens = np.fromiter((len(a) for a in actual[:n]), dtype=np.int64, count=n)
+        flat = (np.fromiter((x for a in actual[:n] for x in a), dtype=np.int64, count=int(lens.sum()))
+                if n else np.zeros(0, np.int64))
+        owner = np.repeat(np.arange(n, dtype=np.int64), lens)
+        base = int(max(pred.max(initial=0), flat.max(initial=0))) + 2    # ids >= -1
+        act_codes = np.unique(owner * base + (flat + 1))
+        self.n_act = np.bincount(act_codes // base, minlength=n) if n else np.zeros(0, np.int64)
+        codes = np.arange(n, dtype=np.int64)[:, None] * base + (pred + 1)
+        self.hit = np.isin(codes, act_codes)
+        if pred.size:                           # set(predicted[i][:k]): a repeated id counts once
+            _, first = np.unique(codes.ravel(), return_index=True)
+            if len(first) != pred.size:
+                once = np.zeros(pred.size, bool)
+                once[first] = True
+                self.hit &= once.reshape(pred.shape)
+        self.csum = np.cumsum(self.hit, axis=1)
+
+    def count(self, k):
+        """len(set(actual[u]) & set(predicted[u][:k])) for every user (int64 [n])."""
+        if self.hit.shape[1] == 0 or k <= 0:
+            return np.zeros(self.hit.shape[0], np.int64)
+        return self.csum[:, min(k, self.hit.shape[1]) - 1]
+
+
+def _precision(h, n, topk):
+    if topk == 0:
+        raise ZeroDivisionError("float division by zero")   # len(...) / float(0)
+    return _seq_sum(h.count(topk) / float(topk)) / n
+
+
+def _recall(h, topk):
+    m = h.n_act != 0
+    return _seq_sum(h.count(topk)[m] / h.n_act[m].astype(np.float64)) / int(m.sum())
+
+
+def _hitrate(h, topk):
+    m = h.n_act != 0
+    return _seq_sum((h.count(topk)[m] > 0).astype(np.float64)) / int(m.sum())
+
 
 def evaluate_mp(positive_list, recommended_list, k_list):      # eval_metrics.py:3-27
-    precision = [precision_at_k(positive_list, recommended_list, k) for k in k_list]
+    h = _Hits(positive_list, recommended_list)
+    n = len(recommended_list)
+    precision = [_precision(h, n, k) for k in k_list]
     print(precision)
-    recall = [recall_at_k(positive_list, recommended_list, k) for k in k_list]
+    recall = [_recall(h, k) for k in k_list]
     print(recall)
-    hit = [hitrate_at_k(positive_list, recommended_list, k) for k in k_list]
+    hit = [_hitrate(h, k) for k in k_list]
     print(hit)
     print("--------")
     return precision, recall, hit
@@ -28,29 +97,12 @@ def precision_at_k_per_sample(actual, predicted, topk):        # eval_metrics.py
 
 
 def precision_at_k(actual, predicted, topk):                   # eval_metrics.py:36-44
-    sum_precision = 0.0
-    num_users = len(predicted)
-    for i in range(num_users):
-        sum_precision += len(set(actual[i]) & set(predicted[i][:topk])) / float(topk)
-    return sum_precision / num_users
+    return _precision(_Hits(actual, predicted), len(predicted), topk)
 
 
 def recall_at_k(actual, predicted, topk):                      # eval_metrics.py:46-56
-    sum_recall, true_users = 0.0, 0
-    for i in range(len(predicted)):
-        act_set = set(actual[i])
-        if len(act_set) != 0:
-            sum_recall += len(act_set & set(predicted[i][:topk])) / float(len(act_set))
-            true_users += 1
-    return sum_recall / true_users
+    return _recall(_Hits(actual, predicted), topk)
 
 
 def hitrate_at_k(actual, predicted, topk):                     # eval_metrics.py:58-69
-    sum_hit, true_users = 0.0, 0
-    for i in range(len(predicted)):
-        act_set = set(actual[i])
-        if len(act_set) != 0:
-            if len(act_set & set(predicted[i][:topk])) > 0:
-                sum_hit += 1
-            true_users += 1
-    return sum_hit / true_users
+    return _hitrate(_Hits(actual, predicted), topk)

@@ -12,14 +12,18 @@ from . import eval_metrics
 from .catalog import score_topk
 
 
-def recommend(model, args, num_users, train_matrix, **kw):
-    """recommended_list of validation.py:9-27: per user, args.topk POI ids, best first."""
+def _recommend_ids(model, args, num_users, train_matrix, **kw):
     model.eval()                                               # validation.py:8
     ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
     nan = int(model._last_nan.item())
     if nan > 0 and type(model).__name__ == "NAIS_basic" and model.report_nan:
         print(nan)                                             # model.py:53-54
-    return ids.cpu().tolist()
+    return ids.cpu().numpy()
+
+
+def recommend(model, args, num_users, train_matrix, **kw):
+    """recommended_list of validation.py:9-27: per user, args.topk POI ids, best first."""
+    return _recommend_ids(model, args, num_users, train_matrix, **kw).tolist()
 
 
 def _metrics(test_positive, val_positive, recommended_list, k_list):
@@ -30,14 +34,14 @@ def _metrics(test_positive, val_positive, recommended_list, k_list):
 
 def NAIS_validation(model, args, num_users, test_positive, val_positive, train_matrix, k_list):
     """validation.py:7-31 (NAIS_basic)."""
-    rec = recommend(model, args, num_users, train_matrix)
+    rec = _recommend_ids(model, args, num_users, train_matrix)
     return _metrics(test_positive, val_positive, rec, k_list)
 
 
 def NAIS_region_validation(model, args, num_users, test_positive, val_positive, train_matrix,
                            businessRegionEmbedList, k_list):
     """validation.py:34-59 (NAIS_regionEmbedding)."""
-    rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList)
+    rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList)
     return _metrics(test_positive, val_positive, rec, k_list)
 
 
@@ -54,10 +58,10 @@ def NAIS_region_distance_validation(model, args, num_users, test_positive, val_p
     """
     _ = args.powerlaw_weight
     if poi_coords is not None:
-        rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
+        rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
                         coords=poi_coords)
     else:
-        rec = recommend(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
+        rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
                         latlon_mat=latlon_mat)
     return _metrics(test_positive, val_positive, rec, k_list)
 
@@ -71,5 +75,5 @@ def new4_validation(model, args, num_users, test_positive, val_positive, train_m
     users are scored normally."""
     model.eval()
     model.extended_tables(nearPOI)
-    rec = recommend(model, args, num_users, train_matrix)
+    rec = _recommend_ids(model, args, num_users, train_matrix)
     return _metrics(test_positive, val_positive, rec, k_list)
