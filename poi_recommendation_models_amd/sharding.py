@@ -76,18 +76,45 @@ def gather_topk(local_users, local_ids, local_scores, num_users, group=None):
     return ids, sc
 
 
-def distributed_recommend(model, args, num_users, train_matrix, group=None, **kw):
-    """recommended_list of validation.py:9-27 computed by all ranks of `group` together."""
+def distributed_plan(csr, num_users, num_pois, k, world, model=None):
+    """"pairs" (column-sharded, distributed_topk_pairs) when the users' histories share POIs
+    (entries >= catalog.PAIR_MIN_SHARING x distinct POIs) and every column block keeps k candidates
+    per user; else "users" (LPT user sharding with replicated tables). With user sharding and
+    shared histories every rank would build the full pair tables; column sharding splits them."""
+    from . import catalog
+    if world < 2 or (model is not None and model._pairs_only):
+        return "pairs" if model is not None and model._pairs_only else "users"
+    hist = csr.hist_len[:num_users]
+    entries = int(hist.sum())
+    used = csr.host_indices[:int(csr.host_indptr[num_users])]
+    distinct = int(np.count_nonzero(np.bincount(used, minlength=num_pois))) if entries else 0
+    S = (num_pois + world - 1) // world
+    if distinct and entries >= catalog.PAIR_MIN_SHARING * distinct and S - int(hist.max(initial=0)) >= k:
+        return "pairs"
+    return "users"
+
+
+def distributed_topk(model, train_matrix, num_users, k, group=None, **kw):
+    """[num_users, k] (ids, scores) of users 0..num_users-1 computed by all ranks of `group`, the
+    same on every rank: column-sharded pairs route or user-sharded per-user kernels
+    (distributed_plan)."""
     import torch.distributed as dist
     from .catalog import device_csr, score_topk
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     model.eval()
     csr = device_csr(train_matrix, model._check_device())
     P = model._item_tables()[0].shape[0]
+    if kw.get("prior") is None and distributed_plan(csr, num_users, P, k, world, model) == "pairs":
+        return distributed_topk_pairs(model, csr, range(num_users), k, group=group, **kw)
     mine = shard_users(csr.hist_len[:num_users], P, world)[rank]
-    ids, sc = score_topk(model, csr, mine, args.topk, **kw)
-    ids, sc = gather_topk(mine, ids, sc, num_users, group=group)
-    return ids.cpu().tolist()
+    ids, sc = score_topk(model, csr, mine, k, **kw)
+    return gather_topk(mine, ids, sc, num_users, group=group)
+
+
+def distributed_recommend(model, args, num_users, train_matrix, group=None, **kw):
+    """recommended_list of validation.py:9-27 computed by all ranks of `group` together."""
+    ids, _ = distributed_topk(model, train_matrix, num_users, args.topk, group=group, **kw)
+    return ids.cpu().numpy()
 
 
 def NAIS_validation_distributed(model, args, num_users, test_positive, val_positive, train_matrix,
