@@ -645,6 +645,16 @@ struct Epi16<HB, false> {          // b1 / w2 read from LDS: acc starts at 0, un
   }
 };
 
+// ReLU folded into |u|: w2 relu(u) = (w2 u + w2 |u|) / 2. The linear part sum_i w2_i u_i =
+// (W1^T w2) . x + w2 . b1 comes from one extra MFMA tile per 32 history items (x3b kernel), so
+// each hidden unit costs one v_fma_f32 with an |acc| source modifier instead of v_max_i32 + v_fma.
+template <int HB>
+struct Epi16A : Epi16<HB, true> {
+  __device__ __forceinline__ float term(int i, float acc, float) const {
+    return this->ws[i] * fabsf(acc);
+  }
+};
+
 template <int DH, int HB, int VAR>
 __global__ void __launch_bounds__(THREADS, 1)
 catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
@@ -910,7 +920,8 @@ struct CfgB {
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
   static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
-                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0) +
+                                  size_t(D + 4) * 4;   // W1^T w2 and w2 . b1 (|u| epilogue)
 };
 
 // NW = waves per workgroup: 8 (2 waves per SIMD, <= 256 VGPRs) for D, H <= 64; 4 (one wave per
@@ -934,6 +945,11 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #define NAIS_X3B_SMFMA 1
 #endif
   constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
+  // |u| epilogue (Epi16A): needs the s-tile machinery and the register-resident b1 / w2 copies
+#ifndef NAIS_X3B_ABS
+#define NAIS_X3B_ABS 0
+#endif
+  constexpr bool ABS = NAIS_X3B_ABS && SMF && EREGS && !DIST;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][hi|lo][NE]
   float* Adist = reinterpret_cast<float*>(ring + 2 * G * 2 * NE);
@@ -942,6 +958,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* hrows = red + 16;
   int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
   double* hco = reinterpret_cast<double*>(hid + JCB);
+  float* vvec = reinterpret_cast<float*>(hco + (DIST ? 2 * JCB : 0));   // [D] W1^T w2, [D] w2 . b1
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   int64_t hbeg, hlen;
@@ -971,7 +988,26 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       wmax = fmaxf(wmax, fabsf(wv[q][x]));
     }
   }
+  if constexpr (ABS) {   // v = W1^T w2 (vvec[0, D)) and c0 = w2 . b1 (vvec[D]), fp32, published below
+    for (int k = tid; k <= D; k += THREADS) {
+      float acc = 0.f;
+      for (int i = 0; i < p.H; ++i)
+        acc = __builtin_fmaf(p.w2[i], k < D ? p.w1[(int64_t)i * p.din + k] : p.b1[i], acc);
+      vvec[k] = acc;
+    }
+  }
   const float Wmax = block_max_n<NW>(wmax, red);
+#ifdef NAIS_X3B_PRIO
+  // static priority for the second-dispatched wave half (cdna_hip_programming.md T5, static form);
+  // readfirstlane keeps the branch scalar so s_setprio runs only on those waves
+  if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
+  float Vmax = 0.f, c0 = 0.f;
+  if constexpr (ABS) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) Vmax = fmaxf(Vmax, fabsf(vvec[k]));
+    c0 = vvec[D];
+  }
   if (DIST) {
     for (int f = tid; f < C::ADIST; f += THREADS) {
       const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
@@ -1031,7 +1067,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 
   float S = 0.f, N = 0.f;
   bool in_hist = false;
-  Epi16<HB, EREGS> epi;
+  typename std::conditional<ABS, Epi16A<HB>, Epi16<HB, EREGS>>::type epi;
 
   // build the fragments of chunk-local item jj into ring slot (grp, it)
   // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
@@ -1067,6 +1103,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   int64_t j0 = 0;   // history chunk base (the step's table-mode write needs it)
   floatx16 sacc;                 // SMF: s tile [32 chunk items x 32 candidates], scaled by Sh*St
   float invShSt = 1.f;
+  floatx16 lacc;                 // ABS: L tile (v . (h_j (.) t_c)), scaled by SL*St
+  float invSLSt = 1.f;
 
   // One pipeline step: the MFMA chain of item `cur` (A_j from the ring slot `src`, t_c from VGPRs)
   // into accN, with the VALU epilogue of the previous item (accP, chunk-local `prev`) cut into KS
@@ -1131,7 +1169,11 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       for (int hb = 0; hb < HB; ++hb) accN[hb] = mfma32(Adist[hb * 64 + lane], fs, accN[hb]);
     }
     const float2 aph = lane_halves(ap);
-    const float a = aph.x + aph.y;
+    float a = aph.x + aph.y;
+    if constexpr (ABS) {   // a = (sum w2 |u| + L) / 2 with L = item pj's row of the L tile + w2 . b1
+      const float2 lh = lane_halves(lacc[((pj >> 3) << 2) | (pj & 3)]);
+      a = 0.5f * (a + ((((pj >> 2) & 1) ? lh.y : lh.x) * invSLSt + c0));
+    }
     float sv;
     if (SMF) {   // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
       const float2 sh2 = lane_halves(sacc[((pj >> 3) << 2) | (pj & 3)]);
@@ -1188,9 +1230,11 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     if (SMF) {
       const float Sh = pow2_scale(Hm);
       invShSt = 1.f / (Sh * St);
+      const float SL = ABS ? pow2_scale(Vmax * Hm) : 1.f;   // |v_k h_k| * SL < 2^14
+      invSLSt = 1.f / (SL * St);
       const int m = lane & 31;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) sacc[r] = lacc[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         float x[8];
@@ -1207,6 +1251,20 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         sacc = mfma16(al, tb_hi[s], sacc);
         sacc = mfma16(ah, tb_lo[s], sacc);
         sacc = mfma16(ah, tb_hi[s], sacc);
+        if constexpr (ABS) {   // the L tile: rows v (.) h_j, same split, same B fragments
+          const float4 v0 = *reinterpret_cast<const float4*>(vvec + hh * DH + 8 * s);
+          const float4 v1 = *reinterpret_cast<const float4*>(vvec + hh * DH + 8 * s + 4);
+          float y[8];
+          y[0] = ok ? (h0.x * v0.x) * SL : 0.f; y[1] = ok ? (h0.y * v0.y) * SL : 0.f;
+          y[2] = ok ? (h0.z * v0.z) * SL : 0.f; y[3] = ok ? (h0.w * v0.w) * SL : 0.f;
+          y[4] = ok ? (h1.x * v1.x) * SL : 0.f; y[5] = ok ? (h1.y * v1.y) * SL : 0.f;
+          y[6] = ok ? (h1.z * v1.z) * SL : 0.f; y[7] = ok ? (h1.w * v1.w) * SL : 0.f;
+          half8 bh, bl;
+          split8(y, bh, bl);
+          lacc = mfma16(bl, tb_hi[s], lacc);
+          lacc = mfma16(bh, tb_lo[s], lacc);
+          lacc = mfma16(bh, tb_hi[s], lacc);
+        }
       }
     }
 #pragma unroll
