@@ -340,6 +340,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     for knob in ("PAIR_FUSED_TOPK", "PAIR_LPT_ORDER"):
         if os.environ.get("NAIS_" + knob):
             setattr(catalog, knob, os.environ["NAIS_" + knob] == "1")
+    if os.environ.get("NAIS_PAIR_TABLE_GATHER_FRAC"):
+        catalog.PAIR_TABLE_GATHER_FRAC = float(os.environ["NAIS_PAIR_TABLE_GATHER_FRAC"])
     if os.environ.get("NAIS_PAIR_FIRST_TABLE_ALL_CUS"):
         catalog.PAIR_FIRST_TABLE_ALL_CUS = os.environ["NAIS_PAIR_FIRST_TABLE_ALL_CUS"] == "1"
     # NAIS_EMULATE_WORLD=N (one process): time rank 0's column shard of an N-GPU run (its tables,
@@ -407,6 +409,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B per
     # entry) + score rows (4 B per user x column; the fused kernel writes only the top-k merges)
     gather_bytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
+    # the timed gather launches are the gather stream's: with PAIR_TABLE_GATHER_FRAC > 0 the table
+    # stream gathers the tail users, so count only the gather stream's share of the entries
+    gather_bytes *= per.get("gather_share", 1.0)
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     table_flops = J * NC * flop_per_pair_item
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -458,6 +463,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "table_cus": table_cus, "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
                 "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
+                "table_gather_frac": catalog.PAIR_TABLE_GATHER_FRAC,
                 "fused_topk": catalog.PAIR_FUSED_TOPK, "lpt_order": catalog.PAIR_LPT_ORDER,
                 **({"emulated_world_shard": emulate} if emulate > 1 and world == 1 else {}),
                 "embed_dim": D, "hidden": H, "h_max": a.h_max, "topk": K,

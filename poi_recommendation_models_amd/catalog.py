@@ -216,6 +216,14 @@ PAIR_FUSED_TOPK = True
 PAIR_LPT_ORDER = True   # users launched in decreasing history length
 PAIR_STRIPE = 256       # columns per gather wave (nais_pairs.hip STRIPE)
 PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
+# Overlapped fused route: the table stream finishes its blocks before the gather stream (config 4:
+# 454 vs 537 ms on 128 CUs each), so after each block's table it also gathers that block for the
+# tail of the (longest-first) user list holding this fraction of the history entries. Each user
+# stays on one stream, so its running top-k still has one writer per launch. Off: the gathers are
+# bound by the memory side, not by their CUs -- at 0 / 0.04 / 0.08 / 0.12 the job took 545.4 /
+# 542.6 / 552.6 / 614.8 ms while the gather stream's own time fell only 539 -> 532 ms
+# (profiles/r1/table_gather_frac/; results bit-identical, test_pairs_blocks_passes_bit_identical).
+PAIR_TABLE_GATHER_FRAC = 0.0
 _masked: dict = {}
 
 
@@ -361,16 +369,19 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             keys = torch.empty(m, k, dtype=torch.int64, device=dev)
             kcount = torch.zeros(m, dtype=torch.int32, device=dev)
 
-            def gather(tab, c0, w, stream_):
+            def gather(tab, c0, w, stream_, a=0, b=None):   # launch slots [a, b) of u_dev
+                b = m if b is None else b
+                if b <= a:
+                    return
                 _capi.check(lib.nais_pair_gather_topk(
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
-                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta), k,
-                    keys.data_ptr(), kcount.data_ptr(), counters[0:1].data_ptr(), stream_),
-                    "nais_pair_gather_topk")
+                    csr.indices.data_ptr(), u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta), k,
+                    keys.data_ptr() + 8 * k * a, kcount.data_ptr() + 4 * a, counters[0:1].data_ptr(),
+                    stream_), "nais_pair_gather_topk")
         else:
             scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
 
-            def gather(tab, c0, w, stream_):
+            def gather(tab, c0, w, stream_, a=0, b=None):
                 _capi.check(lib.nais_pair_gather(
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
@@ -398,6 +409,16 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 ts.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
                 done_g = [None, None]
+                # launch slots [m1, m) are gathered on the table stream (PAIR_TABLE_GATHER_FRAC)
+                m1 = m
+                if fused and PAIR_TABLE_GATHER_FRAC > 0 and m > 1:
+                    hl = csr.hist_len[up[b0:b0 + m]].astype(np.float64)
+                    tail = np.cumsum(hl[::-1])[::-1]        # entries of slots [i, m)
+                    m1 = int(np.searchsorted(-tail, -PAIR_TABLE_GATHER_FRAC * hl.sum(), side="left"))
+                    m1 = min(max(m1, 1), m)
+                if events is not None:
+                    share = float(csr.hist_len[up[b0:b0 + m1]].sum()) / max(1.0, float(csr.hist_len[up[b0:b0 + m]].sum()))
+                    events.append(("gather_share", None, None, share))
             for b, c0 in enumerate(blocks):
                 w = min(W, c1_all - c0)
                 tab = tabs[b % len(tabs)]
@@ -415,11 +436,13 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                             events.append(("table", e_t0, e_t1, 1))
                     e_g0, e_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e_g0.record(gs)
-                    gather(tab, c0, w, gs.cuda_stream)
+                    gather(tab, c0, w, gs.cuda_stream, 0, m1)
                     e_g1.record(gs)
                     done_g[b % 2] = e_g1
                     if events is not None:
                         events.append(("gather", e_g0, e_g1, gather_launches(w)))
+                    if m1 < m:   # the tail users, behind this block's table on the table stream
+                        gather(tab, c0, w, ts.cuda_stream, m1, m)
                     continue
                 timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
                                                          tab[0].data_ptr(), tab[1].data_ptr(), W, st))

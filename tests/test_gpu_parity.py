@@ -517,6 +517,8 @@ def test_pairs_auto_choice_and_new4():
     {"PAIR_FUSED_TOPK": False, "PAIR_MEMORY_FRACTION": 2e-6},   # ... in user passes
     {"PAIR_LPT_ORDER": False},                                  # users in the caller's order
     {"PAIR_LPT_ORDER": False, "PAIR_FUSED_TOPK": False},
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.1},   # tail users on the table stream
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.9, "PAIR_LPT_ORDER": False},
 ])
 def test_pairs_blocks_passes_bit_identical(knobs):
     """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, the
