@@ -42,11 +42,11 @@ namespace {
 #define NAIS_X3B_SCHED 0
 #endif
 #ifndef NAIS_X3B_WIDE
-// 1: the item-side split kernel also for D or H > 64, as 4 waves with one wave per SIMD (512-VGPR
-// budget). Parity-green but slower at D = H = 128 (config 5: 285 vs 386 TF direct, 237 vs 319 TF
-// tables; profiles/r1/cfg5ab/): the per-item A_j build (8 fragments per thread, W1 values held in
-// AGPRs) cannot hide under another wave's MFMAs. 0 (default): the per-pair split kernel there.
-#define NAIS_X3B_WIDE 0
+// 1 (default): the item-side split kernel also for D or H > 64, at 8 waves (2 per SIMD) with one
+// accumulator pass of two hidden blocks at a time and b1 / w2 read from LDS (config 5: direct
+// 369 -> 387 TF, pair tables 319 -> 323 TF on 224 CUs; profiles/r1/cfg5_wide8/). 0: the per-pair
+// split kernel there. (An earlier 4-wave / 512-VGPR form was slower: 285 TF direct.)
+#define NAIS_X3B_WIDE 1
 #endif
 constexpr int WAVES = NAIS_WAVES;           // 512-thread workgroups
 constexpr int THREADS = WAVES * 64;
@@ -645,16 +645,6 @@ struct Epi16<HB, false> {          // b1 / w2 read from LDS: acc starts at 0, un
   }
 };
 
-// ReLU folded into |u|: w2 relu(u) = (w2 u + w2 |u|) / 2. The linear part sum_i w2_i u_i =
-// (W1^T w2) . x + w2 . b1 comes from one extra MFMA tile per 32 history items (x3b kernel), so
-// each hidden unit costs one v_fma_f32 with an |acc| source modifier instead of v_max_i32 + v_fma.
-template <int HB>
-struct Epi16A : Epi16<HB, true> {
-  __device__ __forceinline__ float term(int i, float acc, float) const {
-    return this->ws[i] * fabsf(acc);
-  }
-};
-
 template <int DH, int HB, int VAR>
 __global__ void __launch_bounds__(THREADS, 1)
 catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
@@ -919,13 +909,19 @@ struct CfgB {
   static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);  // build entries per thread
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
+  // PIPE: the epilogue of item j-1 interleaved with item j's MFMAs (two accumulator sets, b1 / w2
+  // in VGPRs) -- fits 256 VGPRs for D, H <= 64. Wider: one accumulator set, epilogue right after
+  // the item's MFMAs (the SIMD's other wave overlaps it), b1 / w2 read from LDS (Epi16<HB, false>).
+#ifdef NAIS_X3B_NOPIPE
+  static constexpr bool PIPE = false;   // debug: the wide epilogue structure for every shape
+#else
+  static constexpr bool PIPE = HB <= 2 && DH <= 32;
+#endif
   static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
-                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0) +
-                                  size_t(D + 4) * 4;   // W1^T w2 and w2 . b1 (|u| epilogue)
+                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
 };
 
-// NW = waves per workgroup: 8 (2 waves per SIMD, <= 256 VGPRs) for D, H <= 64; 4 (one wave per
-// SIMD, up to 512 VGPRs: both pipelined accumulator sets and b1 / w2 stay in registers) above.
+// NW = waves per workgroup (2 per SIMD at 8). D, H <= 64 pipeline the epilogue (CfgB::PIPE).
 template <int DH, int HB, int VAR, int NW>
 __global__ void __launch_bounds__(NW * 64, 1)
 catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
@@ -938,18 +934,13 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   using C = CfgB<DH, HB, DIST, NW>;
   constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
   constexpr int THREADS = NW * 64, CAND_PER_BLOCK = NW * 32;   // shadow the 8-wave defaults
-  constexpr bool EREGS = (HB <= 2 && DH <= 32) || NW == 4;
+  constexpr bool PIPE = C::PIPE;
   // s = h_j . t_c for the chunk's 32 items on the matrix pipe (one 32x32 tile per wave and chunk,
   // the same split-fp16 3-product scheme) instead of a 2*DH-term VALU dot per item and lane
 #ifndef NAIS_X3B_SMFMA
 #define NAIS_X3B_SMFMA 1
 #endif
   constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
-  // |u| epilogue (Epi16A): needs the s-tile machinery and the register-resident b1 / w2 copies
-#ifndef NAIS_X3B_ABS
-#define NAIS_X3B_ABS 0
-#endif
-  constexpr bool ABS = NAIS_X3B_ABS && SMF && EREGS && !DIST;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][hi|lo][NE]
   float* Adist = reinterpret_cast<float*>(ring + 2 * G * 2 * NE);
@@ -958,7 +949,6 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* hrows = red + 16;
   int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
   double* hco = reinterpret_cast<double*>(hid + JCB);
-  float* vvec = reinterpret_cast<float*>(hco + (DIST ? 2 * JCB : 0));   // [D] W1^T w2, [D] w2 . b1
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
   int64_t hbeg, hlen;
@@ -988,26 +978,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       wmax = fmaxf(wmax, fabsf(wv[q][x]));
     }
   }
-  if constexpr (ABS) {   // v = W1^T w2 (vvec[0, D)) and c0 = w2 . b1 (vvec[D]), fp32, published below
-    for (int k = tid; k <= D; k += THREADS) {
-      float acc = 0.f;
-      for (int i = 0; i < p.H; ++i)
-        acc = __builtin_fmaf(p.w2[i], k < D ? p.w1[(int64_t)i * p.din + k] : p.b1[i], acc);
-      vvec[k] = acc;
-    }
-  }
   const float Wmax = block_max_n<NW>(wmax, red);
-#ifdef NAIS_X3B_PRIO
-  // static priority for the second-dispatched wave half (cdna_hip_programming.md T5, static form);
-  // readfirstlane keeps the branch scalar so s_setprio runs only on those waves
-  if (NW == 8 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
-  float Vmax = 0.f, c0 = 0.f;
-  if constexpr (ABS) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) Vmax = fmaxf(Vmax, fabsf(vvec[k]));
-    c0 = vvec[D];
-  }
   if (DIST) {
     for (int f = tid; f < C::ADIST; f += THREADS) {
       const int ln = f & 63, hb = f >> 6, i = hb * 32 + (ln & 31);
@@ -1067,7 +1038,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 
   float S = 0.f, N = 0.f;
   bool in_hist = false;
-  typename std::conditional<ABS, Epi16A<HB>, Epi16<HB, EREGS>>::type epi;
+  // b1 / w2 pre-scaled in VGPRs when pipelined; read from LDS (unscaled, one fma per use) when wide
+  Epi16<HB, PIPE> epi;
 
   // build the fragments of chunk-local item jj into ring slot (grp, it)
   // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
@@ -1103,17 +1075,46 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   int64_t j0 = 0;   // history chunk base (the step's table-mode write needs it)
   floatx16 sacc;                 // SMF: s tile [32 chunk items x 32 candidates], scaled by Sh*St
   float invShSt = 1.f;
-  floatx16 lacc;                 // ABS: L tile (v . (h_j (.) t_c)), scaled by SL*St
-  float invSLSt = 1.f;
 
   // One pipeline step: the MFMA chain of item `cur` (A_j from the ring slot `src`, t_c from VGPRs)
   // into accN, with the VALU epilogue of the previous item (accP, chunk-local `prev`) cut into KS
   // slices placed between the K-steps, so the matrix pipe and the VALU work side by side inside
   // one wave (A/B: profiles/r1/ab_*.json). `live` = false makes the epilogue a no-op (its result
   // is selected away), keeping the control flow uniform inside the step.
-  auto step = [&](auto do_mma, const uint4* src, floatx16 (&accN)[HB], const floatx16 (&accP)[HB],
-                  int cur, int prev, bool live) {
+  // the pair's e and e*s from its attention logit partial ap (and, without SMF, the h.t partial
+  // sd): table-mode stores or the user's running sums
+  auto tail = [&](int pj, float ap, float sd, bool live) {
+    const float2 aph = lane_halves(ap);
+    const float a = aph.x + aph.y;
+    float sv;
+    if (SMF) {   // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
+      const float2 sh2 = lane_halves(sacc[((pj >> 3) << 2) | (pj & 3)]);
+      sv = (((pj >> 2) & 1) ? sh2.y : sh2.x) * invShSt;
+    } else {
+      const float2 sdh = lane_halves(sd);
+      sv = (sdh.x + sdh.y) * invSt;
+    }
+    const bool keep = hid[pj] != (int32_t)c;
+    const float e = expf(a) * (keep ? 1.f : 0.f);
+    if (live) {
+      if (tab.e) {
+        if (valid && hh == 0) {
+          const int64_t o = (hbeg + j0 + pj) * tab.ld + (c - tab.col0);
+          tab_store(tab.e + o, e);
+          tab_store(tab.es + o, e * sv);
+        }
+      } else {
+        in_hist |= !keep;
+        S += e;
+        N += e * sv;
+      }
+    }
+    };
+
+  auto step = [&](auto do_mma, auto do_epi, const uint4* src, floatx16 (&accN)[HB],
+                  const floatx16 (&accP)[HB], int cur, int prev, bool live) {
     constexpr bool MMA = decltype(do_mma)::value;
+    constexpr bool EPIL = decltype(do_epi)::value;
     constexpr int NV = HB * 16;                 // accumulator values per lane
     constexpr int VPS = (NV + KS - 1) / KS;     // epilogue values per K-step slice
     constexpr int QPS = (DH / 4 + KS - 1) / KS; // h . t float4 groups per slice
@@ -1140,10 +1141,12 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
           accN[hb] = mfma16(ah, tb_hi[s], accN[hb]);
         }
       }
+      if constexpr (EPIL) {
 #pragma unroll
-      for (int v = s * VPS; v < (s + 1) * VPS && v < NV; ++v)
-        ap += epi.term(v, accP[v / 16][v % 16], invS);
-      if (!SMF) {
+        for (int v = s * VPS; v < (s + 1) * VPS && v < NV; ++v)
+          ap += epi.term(v, accP[v / 16][v % 16], invS);
+      }
+      if (EPIL && !SMF) {
 #pragma unroll
         for (int q = s * QPS; q < (s + 1) * QPS && q < DH / 4; ++q) {
           const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * q);
@@ -1168,35 +1171,52 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
       for (int hb = 0; hb < HB; ++hb) accN[hb] = mfma32(Adist[hb * 64 + lane], fs, accN[hb]);
     }
-    const float2 aph = lane_halves(ap);
-    float a = aph.x + aph.y;
-    if constexpr (ABS) {   // a = (sum w2 |u| + L) / 2 with L = item pj's row of the L tile + w2 . b1
-      const float2 lh = lane_halves(lacc[((pj >> 3) << 2) | (pj & 3)]);
-      a = 0.5f * (a + ((((pj >> 2) & 1) ? lh.y : lh.x) * invSLSt + c0));
-    }
-    float sv;
-    if (SMF) {   // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
-      const float2 sh2 = lane_halves(sacc[((pj >> 3) << 2) | (pj & 3)]);
-      sv = (((pj >> 2) & 1) ? sh2.y : sh2.x) * invShSt;
-    } else {
-      const float2 sdh = lane_halves(sd);
-      sv = (sdh.x + sdh.y) * invSt;
-    }
-    const bool keep = hid[pj] != (int32_t)c;
-    const float e = expf(a) * (keep ? 1.f : 0.f);
-    if (live) {
-      if (tab.e) {
-        if (valid && hh == 0) {
-          const int64_t o = (hbeg + j0 + pj) * tab.ld + (c - tab.col0);
-          tab_store(tab.e + o, e);
-          tab_store(tab.es + o, e * sv);
+    if constexpr (EPIL) tail(pj, ap, sd, live);
+  };
+
+  // wide shapes (no PIPE): item `cur`'s MFMAs in passes of two 32-unit hidden blocks, each pass's
+  // epilogue right after it (one pass of accumulators live), then the pair's tail
+  auto step_wide = [&](const uint4* src, int cur) {
+    constexpr int HS = HB < 2 ? HB : 2;
+    float ap = 0.f;
+#pragma unroll 1
+    for (int h0 = 0; h0 < HB; h0 += HS) {
+      floatx16 acc[HS];
+#pragma unroll
+      for (int hb = 0; hb < HS; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[hb][r] = epi.init((h0 + hb) * 16 + r);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int hb = 0; hb < HS; ++hb) {
+          const uint4 ahu = src[((h0 + hb) * KS + s) * 64 + lane];
+          const uint4 alu = src[NE + ((h0 + hb) * KS + s) * 64 + lane];
+          const half8 ah = *reinterpret_cast<const half8*>(&ahu);
+          const half8 al = *reinterpret_cast<const half8*>(&alu);
+          acc[hb] = mfma16(al, tb_hi[s], acc[hb]);
+          acc[hb] = mfma16(ah, tb_lo[s], acc[hb]);
+          acc[hb] = mfma16(ah, tb_hi[s], acc[hb]);
         }
-      } else {
-        in_hist |= !keep;
-        S += e;
-        N += e * sv;
+      }
+#pragma unroll
+      for (int hb = 0; hb < HS; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ap += epi.term((h0 + hb) * 16 + r, acc[hb][r], invS);
+    }
+    float sd = 0.f;   // without the s tile (JCB = 64): h_j . t_c as a VALU dot on this lane half
+    if constexpr (!SMF) {
+      const float* hr = hrows + cur * D + hh * DH;
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) {
+        const float4 hv = *reinterpret_cast<const float4*>(hr + 4 * q);
+        sd = __builtin_fmaf(tv[4 * q], hv.x, sd);
+        sd = __builtin_fmaf(tv[4 * q + 1], hv.y, sd);
+        sd = __builtin_fmaf(tv[4 * q + 2], hv.z, sd);
+        sd = __builtin_fmaf(tv[4 * q + 3], hv.w, sd);
       }
     }
+    tail(cur, ap, sd, true);
   };
 
   float SAcur = 1.f;
@@ -1230,11 +1250,9 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     if (SMF) {
       const float Sh = pow2_scale(Hm);
       invShSt = 1.f / (Sh * St);
-      const float SL = ABS ? pow2_scale(Vmax * Hm) : 1.f;   // |v_k h_k| * SL < 2^14
-      invSLSt = 1.f / (SL * St);
       const int m = lane & 31;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[r] = lacc[r] = 0.f;
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         float x[8];
@@ -1251,20 +1269,6 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         sacc = mfma16(al, tb_hi[s], sacc);
         sacc = mfma16(ah, tb_lo[s], sacc);
         sacc = mfma16(ah, tb_hi[s], sacc);
-        if constexpr (ABS) {   // the L tile: rows v (.) h_j, same split, same B fragments
-          const float4 v0 = *reinterpret_cast<const float4*>(vvec + hh * DH + 8 * s);
-          const float4 v1 = *reinterpret_cast<const float4*>(vvec + hh * DH + 8 * s + 4);
-          float y[8];
-          y[0] = ok ? (h0.x * v0.x) * SL : 0.f; y[1] = ok ? (h0.y * v0.y) * SL : 0.f;
-          y[2] = ok ? (h0.z * v0.z) * SL : 0.f; y[3] = ok ? (h0.w * v0.w) * SL : 0.f;
-          y[4] = ok ? (h1.x * v1.x) * SL : 0.f; y[5] = ok ? (h1.y * v1.y) * SL : 0.f;
-          y[6] = ok ? (h1.z * v1.z) * SL : 0.f; y[7] = ok ? (h1.w * v1.w) * SL : 0.f;
-          half8 bh, bl;
-          split8(y, bh, bl);
-          lacc = mfma16(bl, tb_hi[s], lacc);
-          lacc = mfma16(bh, tb_lo[s], lacc);
-          lacc = mfma16(bh, tb_hi[s], lacc);
-        }
       }
     }
 #pragma unroll
@@ -1294,18 +1298,22 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         const int jj = g * G + it;
         if (jj < jn) {
           floatx16 accN[HB];
-          step(std::true_type{}, ring + (((g & 1) * G + it) * 2) * NE, accN, accP, jj, prev,
-               prev >= 0);
+          const uint4* src = ring + (((g & 1) * G + it) * 2) * NE;
+          if constexpr (PIPE) {
+            step(std::true_type{}, std::true_type{}, src, accN, accP, jj, prev, prev >= 0);
 #pragma unroll
-          for (int hb = 0; hb < HB; ++hb) accP[hb] = accN[hb];
-          prev = jj;
+            for (int hb = 0; hb < HB; ++hb) accP[hb] = accN[hb];
+            prev = jj;
+          } else {
+            step_wide(src, jj);
+          }
         }
       }
       __syncthreads();
     }
-    if (prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
+    if (PIPE && prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
       floatx16 accN[HB];
-      step(std::false_type{}, ring, accN, accP, 0, prev, true);
+      step(std::false_type{}, std::true_type{}, ring, accN, accP, 0, prev, true);
     }
   }
   if (tab.e) return;
@@ -1945,8 +1953,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
                                           latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
-    // D, H <= 64: 8 waves (2 per SIMD); larger: 4 waves, one per SIMD, 512-VGPR budget
-    constexpr int NW = (HB <= 2 && DH <= 32) ? WAVES : 4;
+    constexpr int NW = WAVES;
     const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW>::BYTES;
     auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW>;
     static bool attr_set = false;
