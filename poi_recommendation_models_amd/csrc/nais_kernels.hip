@@ -48,6 +48,11 @@ namespace {
 // split kernel there. (An earlier 4-wave / 512-VGPR form was slower: 285 TF direct.)
 #define NAIS_X3B_WIDE 1
 #endif
+#ifndef NAIS_X3B_WIDE_ILV
+// 1: wide shapes build the next group's A_j item by item between this group's MFMA chains
+// instead of all at once before them (A/B; 0 = default)
+#define NAIS_X3B_WIDE_ILV 0
+#endif
 constexpr int WAVES = NAIS_WAVES;           // 512-thread workgroups
 constexpr int THREADS = WAVES * 64;
 constexpr int CAND_PER_BLOCK = WAVES * 32;  // one 32-candidate MFMA column tile per wave
@@ -1286,7 +1291,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     __syncthreads();
     int prev = -1;                      // chunk-local item whose epilogue is pending in accP
     for (int g = 0; g < ngroups; ++g) {
-      if (g + 1 < ngroups) {
+      if ((PIPE || !NAIS_X3B_WIDE_ILV) && g + 1 < ngroups) {
 #pragma unroll
         for (int it = 0; it < G; ++it) {
           const int jj = (g + 1) * G + it;
@@ -1305,6 +1310,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
             for (int hb = 0; hb < HB; ++hb) accP[hb] = accN[hb];
             prev = jj;
           } else {
+            if (NAIS_X3B_WIDE_ILV && g + 1 < ngroups && (g + 1) * G + it < jn)
+              build((g + 1) * G + it, (g + 1) & 1, it);   // next group's A_j beside this MFMA chain
             step_wide(src, jj);
           }
         }
