@@ -35,8 +35,20 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix peak (dense),
 PEAK_F16_MFMA_TFLOPS = 2500.0   # MI355X_MICROARCH.md: BF16/F16 MFMA dense peak, spec
 # the fp16x3 path issues 3 f16 MFMA products per algorithmic fp32 product, so its roof in
 # algorithmic (fp32-equivalent) FLOP/s is the f16 dense peak / 3
-PEAKS = {"fp32": PEAK_FP32_MFMA_TFLOPS, "fp16x3": PEAK_F16_MFMA_TFLOPS / 3,
-         "fp16x3_pairsplit": PEAK_F16_MFMA_TFLOPS / 3}
+# fp16x6 (the fp32-faithful default) issues 6 per algorithmic fp32 product
+PRODUCTS = {"fp32": 1, "fp16x3": 3, "fp16x3_pairsplit": 3, "fp16x6": 6, "fp16x6_pairsplit": 6}
+PEAKS = {k: (PEAK_FP32_MFMA_TFLOPS if v == 1 else PEAK_F16_MFMA_TFLOPS / v) for k, v in PRODUCTS.items()}
+HBM_SPEC_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
+HBM_MEASURED_GBS = 6290.0      # MI355X_MICROARCH.md: float4 copy, measured
+DTYPES = {
+    "fp32": "fp32 (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulate)",
+    "fp16x6": "fp32-faithful: W1 x products as 6 f16 MFMA products of exact hi/mid/lo fp16 splits "
+              "(dropped terms <= ~2^-33 relative, below fp32 rounding), fp32 accumulate; all other "
+              "arithmetic fp32",
+    "fp16x6_pairsplit": "fp32-faithful (fp16x6 arithmetic, per-pair split of x = h . t)",
+    "fp16x3": "narrower than fp32: W1 x products as 3 f16 MFMA products of hi/lo splits (~2^-21)",
+    "fp16x3_pairsplit": "narrower than fp32: fp16x3 arithmetic, per-pair split",
+}
 
 
 def parse():
@@ -54,11 +66,16 @@ def parse():
     ap.add_argument("--hidden", type=int, default=64)
     ap.add_argument("--h-max", type=int, default=200)
     ap.add_argument("--topk", type=int, default=50)
-    ap.add_argument("--precision", default="fp16x3", choices=["fp32", "fp16x3", "fp16x3_pairsplit"])
+    ap.add_argument("--precision", default="fp16x6", choices=sorted(PRODUCTS))
     ap.add_argument("--no-fp32-leg", action="store_true",
-                    help="skip the extra exact-fp32 timing reported under 'fp32_path'")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+                    help="skip the secondary exact-fp32 and fp16x3 timings ('fp32_path', 'fp16x3_path')")
+    ap.add_argument("--leg-steps", type=int, default=3, help="timed steps of each secondary leg")
+    ap.add_argument("--cpu-users", type=int, default=32,
+                    help="CPU baseline sample: the first N users (after a 1-user warm-up)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="cap on the CPU sample's time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-self-check", action="store_true",
+                    help="skip the oracle check of 2 bench users' top-50 after the timed steps")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse N>1 on one GPU")
@@ -68,26 +85,87 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(p, data, users, k, seconds):
-    """The CPU restatement (oracle, numpy fp32 + BLAS threads) on a bounded user sample."""
-    from oracle import nais_oracle
+def cpu_threads():
+    """CPUs this process may use: the affinity set, capped by a cgroup quota and OMP_NUM_THREADS
+    (os.cpu_count() shows the whole machine on the GPU boxes)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
     except Exception:
-        cores = os.cpu_count()
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(p, data, users, k, seconds):
+    """the torch-CPU restatement of the reference's evaluation loop
+    (oracle/torch_cpu.py: candidate rows, 1,024-row forward chunks, torch.topk), all usable
+    cores, a 1-user warm-up, then the listed users (the first 32) until `seconds` run out."""
+    from oracle import torch_cpu
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    m = torch_cpu.TorchNAIS(p)
+    torch_cpu.recommend_user(m, data.history(int(users[0])), data.num_pois, k)      # warm-up
     pairs, t0, n = 0, time.perf_counter(), 0
     for u in users:
-        cand, sc = nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois)
-        nais_oracle.topk_ids(cand, sc, k)
-        pairs += len(cand)
+        pairs += torch_cpu.recommend_user(m, data.history(int(u)), data.num_pois, k)[2]
         n += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": pairs / dt, "unit": "pairs/s", "cores": int(cores), "kind": "port",
-            "sample": f"{n} users of the same workload (complement candidates + chunked forward + "
-                      f"top-{k}, oracle/nais_oracle.py numpy fp32), {pairs} pairs in {dt:.1f} s"}
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"users {int(users[0])}..{int(users[n - 1])} ({n} users, after a 1-user warm-up) "
+                      f"of the same workload: complement candidate rows + 1,024-row forward chunks + "
+                      f"torch.topk(50), oracle/torch_cpu.py (torch {torch.__version__} CPU, "
+                      f"{threads} threads), {pairs} pairs in {dt:.1f} s"}
+
+
+def self_check(p, data, users, ids, sc, k):
+    """Oracle check of the timed path's output for a few users (numpy restatement, test
+    infrastructure): every returned id's oracle score within 1e-4 of ours, and the returned set
+    equal to the oracle's top-k up to runs of scores within 4 fp32 ulps at the cut."""
+    from oracle import nais_oracle
+    out = {"users": [], "max_abs_score_diff": 0.0, "topk_ok": True}
+    for u in users:
+        cand, ref = nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois, chunk=4096)
+        lut = dict(zip(cand.tolist(), ref.tolist()))
+        got = np.array([lut[int(c)] for c in ids[u]])
+        out["max_abs_score_diff"] = max(out["max_abs_score_diff"], float(np.max(np.abs(got - sc[u]))))
+        rid, rsc = nais_oracle.topk_ids(cand, ref, k)
+        cut = float(rsc[-1]) - 4 * float(np.spacing(np.float32(abs(rsc[-1]))))
+        extra = set(ids[u].tolist()) - set(rid.tolist())
+        ok = all(lut[c] >= cut for c in extra) and out["max_abs_score_diff"] <= 1e-4
+        out["topk_ok"] = out["topk_ok"] and ok
+        out["users"].append(int(u))
+    return out
+
+
+def self_launch(a):
+    """--gpus N > 1 without a torchrun environment: start N fresh worker processes through
+    torch.distributed.run (this process never touches the GPU) and return their exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def main():
@@ -97,11 +175,13 @@ def main():
         if a.users_per_step == 256:
             a.users_per_step = 64
         a.no_cpu_baseline = True   # the CPU leg is quoted on the metric config (4)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(a))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     if a.gpus != world:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     import torch.distributed as dist
@@ -276,7 +356,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            cpu = cpu_baseline(p_host, data, mine[:64], K, a.cpu_seconds)
+            cpu = cpu_baseline(p_host, data, np.arange(a.cpu_users), K, a.cpu_seconds)
         out = {
             "metric": "scored (user,POI) pairs/sec full-catalog + top-50, %s POIs"
                       % ("100k" if a.config == 4 else "1M"),
@@ -289,8 +369,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if a.precision == "fp32" else
-                     "fp32 (W1 x products as 3 fp16 MFMA products of power-of-two-scaled hi/lo splits, fp32 accumulate)",
+            "dtype": DTYPES[a.precision],
             "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
             "config": {
                 "workload": ("config4 Gowalla-scale" if a.config == 4 else
@@ -305,13 +384,14 @@ def main():
             },
             "roofline": {
                 "kernel": ("catalog_score_kernel" if a.precision == "fp32" else
-                           "catalog_score_x3b_kernel" if (D <= 64 and H <= 64 and a.precision == "fp16x3")
-                           else "catalog_score_x3_kernel") + " (nais_score_catalog)",
+                           "catalog_score_x3_kernel" if "pairsplit" in a.precision
+                           else "catalog_score_x3b_kernel") + " (nais_score_catalog)",
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": peak,
                 "peak_basis": ("fp32 MFMA dense" if a.precision == "fp32" else
-                               "f16 MFMA dense 2.5 PF / 3 products per algorithmic fp32 product"),
+                               "f16 MFMA dense 2.5 PF / %d products per algorithmic fp32 product"
+                               % PRODUCTS[a.precision]),
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
                 "traffic": traffic,
@@ -330,7 +410,7 @@ def main():
 def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
     from poi_recommendation_models_amd import catalog
-    from poi_recommendation_models_amd.sharding import distributed_topk_pairs
+    from poi_recommendation_models_amd.sharding import column_blocks, distributed_topk_pairs
     if os.environ.get("NAIS_PAIR_TABLE_CUS"):          # A/B knobs of the table/gather overlap
         catalog.PAIR_TABLE_CUS = int(os.environ["NAIS_PAIR_TABLE_CUS"])
     if os.environ.get("NAIS_PAIR_CU_LAYOUT"):
@@ -350,6 +430,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
     users = np.arange(a.num_users)
     group = None
+    last = {}
     if world == 1:   # the same code path with a trivial process group is not needed: call direct
         from poi_recommendation_models_amd.catalog import _score_topk_pairs
 
@@ -372,11 +453,15 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(nsteps):
-            job(evs[i])
+            last["out"] = job(evs[i])
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
         per, nl = {}, {}
         for step_ev in evs:
             for kind, e0, e1, launches in step_ev:
@@ -389,59 +474,115 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         return el, per
 
     elapsed, per = run(a.precision, a.warmup, a.steps)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     pairs_job = float((P - hist_len[users]).sum())            # every user's whole catalog
-    S = (P + world - 1) // world
     if emulate > 1 and world == 1:
-        S = (P + emulate - 1) // emulate
+        c0, c1 = column_blocks(P, emulate)[0]
         pairs_job /= emulate     # ~ the shard's share (value is then a per-rank rate estimate)
-    c0, c1 = min(rank * S, P), min((rank + 1) * S, P)
+    else:
+        c0, c1 = column_blocks(P, world)[rank]
     NC = c1 - c0
     entries = int(hist_len.sum())
     J = int(np.count_nonzero(np.bincount(data.indices, minlength=P)))
-    # algorithmic work per step on this rank
     fused = catalog.PAIR_FUSED_TOPK and K <= 256
     Wb, st_w = catalog.PAIR_BLOCK_COLS, catalog.PAIR_STRIPE
     stripes = sum((min(Wb, NC - b) + st_w - 1) // st_w for b in range(0, NC, Wb))
-    # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B per
-    # entry) + score rows (4 B per user x column; the fused kernel writes only the top-k merges)
-    gather_bytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
-    # the timed gather launches are the gather stream's: with PAIR_TABLE_GATHER_FRAC > 0 the table
-    # stream gathers the tail users, so count only the gather stream's share of the entries
-    gather_bytes *= per.get("gather_share", 1.0)
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
-    table_flops = J * NC * flop_per_pair_item
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    table_cus = per.get("table_cus", ncu) or ncu
-    g_ms = sum(per.get("gather", [])) / a.steps
-    t_ms = sum(per.get("table", [])) / a.steps
+
+    def kernels(per, precision):
+        """(gather roofline dict, table roofline dict) of one leg's per-step event timings."""
+        # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B
+        # per entry) + score rows (4 B per user x column; the fused kernel writes only the top-k
+        # merges); with PAIR_TABLE_GATHER_FRAC > 0 only the gather stream's share is timed
+        gbytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
+        gbytes *= per.get("gather_share", 1.0)
+        g_ms = sum(per.get("gather", [])) / a_steps[precision]
+        t_ms = sum(per.get("table", [])) / a_steps[precision]
+        n_gl = max(1, per["_launches"].get("gather", 0) // a_steps[precision])
+        table_cus = per.get("table_cus", ncu) or ncu
+        tflops = J * NC * flop_per_pair_item
+        g_ach = gbytes / (g_ms * 1e-3) / 1e9 if g_ms else None
+        t_ach = tflops / (t_ms * 1e-3) / 1e12 if t_ms else None
+        gather = {
+            "kernel": "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
+                      "pair_gather_kernel (nais_pair_gather)",
+            "bound": "hbm", "achieved": g_ach, "peak": HBM_SPEC_GBS, "unit": "GB/s",
+            "frac": g_ach / HBM_SPEC_GBS if g_ach else None,
+            "frac_of_measured_hbm": g_ach / HBM_MEASURED_GBS if g_ach else None,
+            "measured_hbm_peak": HBM_MEASURED_GBS,
+            "served_from": "Infinity Cache (MALL) mostly: the 256-column stripe of the tables "
+                           "(J x 256 x 8 B ~ 205 MB) fits the 256 MB MALL, so the memory side "
+                           "delivers more than the HBM copy rate",
+            "algorithmic_bytes_per_launch": gbytes / n_gl, "avg_launch_ms": g_ms / n_gl,
+            "launches_per_step": n_gl, "ms_per_step": g_ms, "cus": ncu - table_cus if table_cus < ncu else ncu,
+        }
+        table = {
+            "kernel": "catalog_score_x3b_kernel in table mode (nais_pair_table)" if precision != "fp32"
+                      else "catalog_score_kernel in table mode (nais_pair_table)",
+            "bound": "mfma", "achieved": t_ach, "peak": PEAKS[precision], "unit": "TFLOP/s",
+            "frac": t_ach / PEAKS[precision] if t_ach else None,
+            "frac_of_its_cus": t_ach / (PEAKS[precision] * table_cus / ncu) if t_ach else None,
+            "peak_basis": ("fp32 MFMA dense" if precision == "fp32" else
+                           "f16 MFMA dense 2.5 PF / %d products per algorithmic fp32 product"
+                           % PRODUCTS[precision]),
+            "algorithmic_flop_per_step": tflops, "ms_per_step": t_ms, "cus": table_cus,
+            "launches_per_step": per["_launches"].get("table", 0) // a_steps[precision],
+        }
+        return gather, table
+
+    a_steps = {a.precision: a.steps}
+    gather, table = kernels(per, a.precision)
     k_ms = sum(per.get("topk", [])) / a.steps
-    n_gl = max(1, per["_launches"].get("gather", 0) // a.steps)
-    achieved = gather_bytes / (g_ms * 1e-3) / 1e9
-    traffic = None
+    # the roofline line is the kernel on the job's critical path (the longer of the two streams)
+    dominant = table if (table["ms_per_step"] or 0) > (gather["ms_per_step"] or 0) else gather
+    other = gather if dominant is table else table
     try:
-        tj = json.load(open(a.traffic_json)).get("pairs_gather_topk" if fused else "pairs_gather", {})
-        if (tj.get("num_users") == a.num_users and tj.get("num_pois") == P and tj.get("world") == world
-                and tj.get("block_cols") == catalog.PAIR_BLOCK_COLS):
-            traffic = tj.get("hbm_bytes_per_launch")
+        tj = json.load(open(a.traffic_json))
+        key = ("pairs_gather_topk" if fused else "pairs_gather") if dominant is gather else \
+            "pairs_table_" + a.precision
+        e = tj.get(key, {})
+        ok = (e.get("num_users") == a.num_users and e.get("num_pois") == P and e.get("world") == world
+              and e.get("block_cols") == catalog.PAIR_BLOCK_COLS
+              and e.get("precision", a.precision) == a.precision)
+        dominant["traffic"] = e.get("hbm_bytes_per_launch") if ok else None
+        if ok and dominant is table:
+            dominant["traffic_note"] = "per launch (one 512-column table block)"
     except Exception:
-        pass
-    fp32_leg = None
-    if world == 1 and not a.no_fp32_leg and a.precision != "fp32":
-        el32, per32 = run("fp32", 0, 1)
-        t32 = sum(per32.get("table", []))
-        fp32_leg = {"precision": "fp32 (v_mfma_f32_32x32x2_f32 tables, exact fp32)", "value": pairs_job / el32,
-                    "unit": "pairs/s", "steps": 1, "table_ms": t32,
-                    "table_tflops": table_flops / (t32 * 1e-3) / 1e12, "peak": PEAK_FP32_MFMA_TFLOPS}
+        dominant["traffic"] = None
+    if "traffic" not in dominant:
+        dominant["traffic"] = None
+    dominant["note"] = ("gather: algorithmic bytes per launch (one 256-column stripe) = sum_u h_u x "
+                        "columns x 8 B table reads + 12 B CSR id + row map per history entry; table: "
+                        "SURVEY.md 8(d) FLOP per (pair, history item) x distinct history POIs x "
+                        "columns; traffic = rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per launch")
+    dominant["overlap"] = ("tables on CUs [0, %d) and gathers on the other %d, side by side on "
+                           "CU-masked streams (double-buffered tables)" % (table["cus"], ncu - table["cus"])
+                           if table["cus"] < ncu else "serial")
+    dominant["other_kernel"] = other
+    dominant["topk_ms_per_step"] = k_ms
+    legs = {}
+    if world == 1 and not a.no_fp32_leg:
+        for prec in ("fp32", "fp16x3"):
+            if prec == a.precision:
+                continue
+            a_steps[prec] = a.leg_steps
+            el_l, per_l = run(prec, 1, a.leg_steps)
+            g_l, t_l = kernels(per_l, prec)
+            legs[prec] = {"precision": DTYPES[prec], "value": pairs_job * a.leg_steps / el_l,
+                          "unit": "pairs/s", "steps": a.leg_steps, "warmup": 1,
+                          "ms_per_step": el_l / a.leg_steps * 1e3,
+                          "table_ms_per_step": t_l["ms_per_step"], "table_tflops": t_l["achieved"],
+                          "table_peak_tflops": t_l["peak"], "table_cus": t_l["cus"],
+                          "gather_ms_per_step": g_l["ms_per_step"]}
         model.precision = a.precision
+    check = None
+    if world == 1 and emulate == 1 and not a.no_self_check and rank == 0:
+        ids, sc = last["out"]
+        check = self_check(p_host, data, [1, 4242 % a.num_users], ids.cpu().numpy(), sc.cpu().numpy(), K)
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
-            rng = np.random.default_rng(100)
-            cpu = cpu_baseline(p_host, data, rng.choice(users, 64, replace=False), K, a.cpu_seconds)
+            cpu = cpu_baseline(p_host, data, np.arange(a.cpu_users), K, a.cpu_seconds)
         out = {
             "metric": "scored (user,POI) pairs/sec full-catalog + top-50, 100k POIs",
             "value": pairs_job * a.steps / elapsed,
@@ -453,14 +594,16 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32" if a.precision == "fp32" else
-                     "fp32 (W1 x products as 3 fp16 MFMA products of power-of-two-scaled hi/lo splits, fp32 accumulate)",
+            "dtype": DTYPES[a.precision],
             "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
+            "world_size": world,
+            "backend": (a.backend if world > 1 else None),
             "config": {
                 "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
                             "score + top-%d; one step = every user's whole catalog" % (a.num_users, P, D, K),
-                "model": "NAIS_basic", "strategy": "pairs", "num_users": a.num_users, "num_pois": P,
-                "table_cus": table_cus, "cu_layout": catalog.PAIR_CU_LAYOUT,
+                "model": "NAIS_basic", "strategy": "pairs", "precision": a.precision,
+                "num_users": a.num_users, "num_pois": P,
+                "table_cus": table["cus"], "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
                 "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
                 "table_gather_frac": catalog.PAIR_TABLE_GATHER_FRAC,
@@ -471,37 +614,11 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "parallelism": f"POI columns sharded over {world} GPU(s) (all users per rank), "
                                "tables replicated, one all-gather + merge of the top-k blocks",
             },
-            "roofline": {
-                "kernel": "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
-                          "pair_gather_kernel (nais_pair_gather)",
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": 8000.0,
-                "unit": "GB/s",
-                "frac": achieved / 8000.0,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": gather_bytes / n_gl,
-                "avg_launch_ms": g_ms / n_gl,
-                "launches_per_step": n_gl,
-                "note": "algorithmic bytes per launch (one 256-column stripe for the fused kernel) = "
-                        "sum_u h_u x columns x 8 B table reads + 12 B CSR id + row map per history "
-                        "entry (+ 4 B score writes per user x column, non-fused); traffic = "
-                        "rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per launch, Infinity-Cache hits "
-                        "included",
-                "overlap": "tables on CUs [0, %d) and gathers on the other %d, side by side on "
-                           "CU-masked streams (double-buffered tables)" % (table_cus, ncu - table_cus)
-                           if table_cus < ncu else "serial",
-                "table_kernel": {"name": "catalog_score_x3b_kernel in table mode (nais_pair_table)",
-                                 "bound": "mfma", "ms_per_step": t_ms, "cus": table_cus,
-                                 "frac_of_its_cus": (table_flops / (t_ms * 1e-3) / 1e12) /
-                                                    (PEAKS[a.precision] * table_cus / ncu) if t_ms else None,
-                                 "achieved_tflops": table_flops / (t_ms * 1e-3) / 1e12 if t_ms else None,
-                                 "peak_tflops": PEAKS[a.precision],
-                                 "frac": (table_flops / (t_ms * 1e-3) / 1e12) / PEAKS[a.precision] if t_ms else None},
-                "topk_ms_per_step": k_ms,
-            },
+            "roofline": dominant,
             "cpu_baseline": cpu,
-            "fp32_path": fp32_leg,
+            "self_check": check,
+            "fp32_path": legs.get("fp32"),
+            "fp16x3_path": legs.get("fp16x3"),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -51,6 +51,11 @@ extern "C" {
                                           operands A_j = W1 diag(h_j) (split once per item) and t_c     */
 #define NAIS_PRECISION_FP16X3_PAIRSPLIT 2 /* same arithmetic class, splitting x = h_j (.) t_c per pair
                                           (the reference's operand order; more VALU work)                 */
+#define NAIS_PRECISION_FP16X6 3        /* fp32-faithful split (the default): hi/mid/lo fp16 pieces hold
+                                          every operand exactly, 6 f16 MFMA products per fp32 product
+                                          (dropped terms <= ~2^-33 relative, below fp32's 2^-24 product
+                                          rounding), fp32 accumulate; item-side operands as FP16X3     */
+#define NAIS_PRECISION_FP16X6_PAIRSPLIT 4 /* FP16X6 arithmetic on the per-pair split of x = h_j (.) t_c */
 
 /* flags for nais_forward */
 #define NAIS_FLAG_SIGMOID 1            /* apply sigmoid (model.py:55); else return the logits of attention_network */

@@ -1,0 +1,66 @@
+"""TEST / BASELINE INFRASTRUCTURE ONLY -- never imported by the product package.
+
+A torch-CPU restatement of the reference's full-catalog evaluation of NAIS_basic, used as the
+CPU baseline of bench.py and pinned against the reference's own golden
+outputs (tests/test_torch_cpu_baseline.py). It follows the reference's operations and their
+order in plain torch ops on the CPU, with torch's intra-op threads:
+
+  candidates   batches.py:52-65  complement of the CSR history, ascending; the history row
+                                 repeated once per candidate (a [C, h] int64 matrix)
+  forward      model.py:40-89    gather -> h * t -> attn_layer1 -> ReLU (Dropout off in eval)
+                                 -> attn_layer2 -> exp -> mask -> sum -> pow(beta) -> divide ->
+                                 weight the history rows -> bmm with t -> sum -> sigmoid
+  loop         validation.py:9-27 1,024-candidate chunks, torch.cat, torch.topk(pred, k)
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+class TorchNAIS:
+    """NAIS_basic's eval-mode forward (model.py:40-89) on CPU tensors."""
+
+    def __init__(self, params, beta=0.5):
+        t = lambda k: torch.as_tensor(np.ascontiguousarray(params[k]), dtype=torch.float32)
+        self.eh, self.et = t("embed_history.weight"), t("embed_target.weight")
+        self.w1, self.b1, self.w2 = t("attn_layer1.weight"), t("attn_layer1.bias"), t("attn_layer2.weight")
+        self.beta = beta
+
+    @torch.no_grad()
+    def __call__(self, user_history, target_item):
+        history = self.eh[user_history]                                   # model.py:64 (b, n, d)
+        target = self.et[target_item]                                     # model.py:66
+        b = len(target)
+        target = target.reshape(b, 1, -1)
+        x = history * target                                              # model.py:70
+        r1 = torch.relu(torch.nn.functional.linear(x, self.w1, self.b1))  # model.py:71 (eval)
+        r2 = torch.nn.functional.linear(r1, self.w2)                      # model.py:73
+        e = torch.exp(r2).squeeze(-1)                                     # model.py:75-76
+        e = e * (user_history != target_item.reshape(b, 1))               # model.py:77-78, 92-95
+        s = torch.pow(torch.sum(e, dim=-1), self.beta)                    # model.py:79-80
+        w = torch.divide(e.T, s).T.reshape(b, -1, 1)                      # model.py:82-83
+        res = history * w                                                 # model.py:84
+        pred = torch.bmm(res, target.reshape(b, -1, 1)).squeeze(-1)       # model.py:86-87
+        return torch.sigmoid(torch.sum(pred, dim=-1))                     # model.py:88, 55
+
+
+def candidates(history, num_pois):
+    """batches.py:56-57: ascending complement, the history repeated per candidate."""
+    keep = np.ones(num_pois, dtype=bool)
+    keep[np.asarray(history, dtype=np.int64)] = False
+    cand = np.nonzero(keep)[0]
+    rows = np.repeat(np.asarray(history, dtype=np.int64)[None, :], len(cand), axis=0)
+    return torch.from_numpy(rows), torch.from_numpy(cand)
+
+
+def recommend_user(model, history, num_pois, k, chunk=1024):
+    """validation.py:11-27 for one user: (top-k POI ids, their scores, #candidates)."""
+    user_history, target_list = candidates(history, num_pois)
+    n = math.ceil(len(user_history) / chunk)
+    pred = torch.cat([model(user_history[chunk * i:chunk * (i + 1)],
+                            target_list[chunk * i:chunk * (i + 1)]) for i in range(n)], dim=-1)
+    vals, idx = torch.topk(pred, k)
+    return target_list[idx].numpy(), vals.numpy(), len(target_list)

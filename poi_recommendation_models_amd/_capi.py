@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, LIB_NAME)
 
 ABI_VERSION = 6
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
+PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE, VARIANT_DISTANCE = 0, 1, 2, 3
 FLAG_SIGMOID = 1
 

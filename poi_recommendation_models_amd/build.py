@@ -25,18 +25,38 @@ def build(force=False, extra=(), out=None):
     if out is not None:
         force = True
     OUT_ = out or OUT
-    deps = [*SRCS, os.path.join(HERE, "csrc", "nais_internal.h"), os.path.join(ROOT, "include", "nais.h")]
+    csrc = os.path.join(HERE, "csrc")
+    deps = [*SRCS, os.path.join(ROOT, "include", "nais.h"),
+            *(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".h", ".hip")))]
     if not force and os.path.exists(OUT_) and all(os.path.getmtime(OUT_) >= os.path.getmtime(d) for d in deps):
         return OUT_
     # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds/muls into v_pk_*_f32, which
     # cost more issue slots than two scalar ops beside MFMAs (cdna_hip_programming.md, price table);
     # measured +5 % on the split-fp16 catalog kernel (profiles/r1/ab_*.json).
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-fno-slp-vectorize",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT_ + ".tmp", *SRCS, *extra]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError(f"hipcc failed ({r.returncode}): {' '.join(cmd)}")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize",
+             "-I", os.path.join(ROOT, "include"), *extra]
+    # one object per translation unit, compiled in parallel, then one link
+    objs = [OUT_ + "." + os.path.basename(s) + ".o" for s in SRCS]
+    procs = [(subprocess.Popen([hipcc(), *flags, "-c", "-o", o, s], stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, text=True), s) for s, o in zip(SRCS, objs)]
+    failed = []
+    for pr, s in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            sys.stderr.write(out)
+            failed.append(os.path.basename(s))
+    try:
+        if failed:
+            raise RuntimeError(f"hipcc failed on {failed}")
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_ + ".tmp", *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError(f"hipcc link failed ({r.returncode}): {' '.join(cmd)}")
+    finally:
+        for o in objs:
+            if os.path.exists(o):
+                os.remove(o)
     os.replace(OUT_ + ".tmp", OUT_)
     return OUT_
 

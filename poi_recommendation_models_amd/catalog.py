@@ -134,8 +134,23 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     `strategy` (default: the model's `catalog_strategy`, "auto"): "direct" runs the fused per-user
     kernels; "pairs" computes each (distinct history POI, candidate) term once and gathers every
     user's sums from those tables (nais_pair_*); "auto" picks "pairs" when the users' history
-    entries outnumber their distinct POIs by PAIR_MIN_SHARING and there is no prior."""
+    entries outnumber their distinct POIs by PAIR_MIN_SHARING and there is no prior.
+
+    `stream` (a raw hipStream_t handle): the whole call -- its allocations, uploads, kernels and
+    the final reorder -- runs on that stream, which first waits for the caller's current stream;
+    the current stream then waits for it before the results are returned."""
     dev = model._check_device()
+    if stream is not None:
+        ext = torch.cuda.ExternalStream(stream, device=dev)
+        cur = torch.cuda.current_stream(dev)
+        ext.wait_stream(cur)
+        with torch.cuda.stream(ext):
+            out = score_topk(model, train_matrix, users, k, region_of, coords, latlon_mat, ordered,
+                             None, prior, strategy)
+        cur.wait_stream(ext)
+        for t in out:
+            t.record_stream(cur)
+        return out
     strategy = strategy or getattr(model, "catalog_strategy", "auto")
     if strategy not in ("auto", "direct", "pairs"):
         raise ValueError(f"unknown strategy {strategy!r}")
@@ -234,8 +249,9 @@ def auto_table_cus(model, J, NC, entries, ncu):
     to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 128 of 256,
     config 5: 224)."""
     H, din = model.attn_layer1.weight.shape
-    split = getattr(model, "precision", "fp16x3") != "fp32"
-    t_tab = J * NC * 2.0 * H * din * (3 if split else 1) / (1.1e15 if split else 1.3e14)
+    prec = getattr(model, "precision", "fp16x6")
+    products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
+    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else 1.1e15)
     gbytes = entries * NC * 8.0
     xcd = max(1, ncu // 8)
     best, best_t = ncu // 2, None

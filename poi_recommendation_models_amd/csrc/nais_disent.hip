@@ -45,7 +45,7 @@ __device__ __forceinline__ float mlp(const float* x, const float* w1, const floa
     const float* wr = w1 + int64_t(i) * D;
     for (int d = 0; d < D; ++d) a = fmaf(wr[d], x[d], a);
     a += b1[i];
-    part = fmaf(w2[i], fmaxf(a, 0.f), part);
+    part = fmaf(w2[i], nais_relu(a), part);
   }
   return wsum(part);
 }

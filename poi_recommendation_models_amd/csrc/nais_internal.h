@@ -7,3 +7,6 @@
 __attribute__((visibility("hidden"))) int nais_internal_fail(int code, const char* msg);
 // NAIS_E_HIP (with the HIP error text) if the last launch failed, else NAIS_OK.
 __attribute__((visibility("hidden"))) int nais_internal_check_launch(const char* what);
+
+// ReLU that keeps NaN, as torch.relu (model.py:71): fmaxf / v_max_f32 would return 0 for a NaN.
+__device__ __forceinline__ float nais_relu(float v) { return (v < 0.f) ? 0.f : v; }

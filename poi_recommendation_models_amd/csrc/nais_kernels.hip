@@ -569,6 +569,72 @@ __device__ __forceinline__ void split8(const float (&x)[8], half8& hi, half8& lo
   lo = *reinterpret_cast<const half8*>(&lu);
 }
 
+// x -> (hi, mid, lo), x == hi + mid + lo exactly for the scaled operands of this file (33
+// significant bits >= fp32's 24; f16 subnormals only below 2^-37 of the scaled maximum):
+//   hi = f16(x),  r = x - hi (exact, v_fma_mix_f32),  mid = f16(r),  lo = f16(r - mid) (exact
+//   subtraction inside v_fma_mix{lo,hi}_f16). The fp16x6 path multiplies such splits (6 products).
+__device__ __forceinline__ void split8_3(const float (&x)[8], half8& hi, half8& mid, half8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) hi[e] = (_Float16)x[e];
+  const uint4 hu = *reinterpret_cast<const uint4*>(&hi);
+  const uint32_t hw[4] = {hu.x, hu.y, hu.z, hu.w};
+  float r[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    asm("v_fma_mix_f32 %0, -%2, 1.0, %3 op_sel_hi:[1,0,0]\n\t"
+        "v_fma_mix_f32 %1, -%2, 1.0, %4 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+        : "=&v"(r[2 * q]), "=&v"(r[2 * q + 1])
+        : "v"(hw[q]), "v"(x[2 * q]), "v"(x[2 * q + 1]));
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) mid[e] = (_Float16)r[e];
+  const uint4 mu = *reinterpret_cast<const uint4*>(&mid);
+  uint32_t l0, l1, l2, l3;
+  asm("v_fma_mixlo_f16 %0, -%4, 1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, -%4, 1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, -%5, 1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%5, 1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %2, -%6, 1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %2, -%6, 1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %3, -%7, 1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %3, -%7, 1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(mu.x), "v"(mu.y), "v"(mu.z), "v"(mu.w), "v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]),
+        "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+  const uint4 lu = make_uint4(l0, l1, l2, l3);
+  lo = *reinterpret_cast<const half8*>(&lu);
+}
+
+// NPC split pieces of 8 fp32 values: 2 = (hi, lo) for fp16x3, 3 = (hi, mid, lo) for fp16x6
+template <int NPC>
+__device__ __forceinline__ void split_pieces(const float (&x)[8], half8 (&pc)[NPC]) {
+  if constexpr (NPC == 2) split8(x, pc[0], pc[1]);
+  else split8_3(x, pc[0], pc[1], pc[2]);
+}
+
+// c += a . b over the pieces, smallest terms first:
+//   NPC = 2 (fp16x3): al*bh + ah*bl + ah*bh       -- al*bl (~2^-22 relative) dropped
+//   NPC = 3 (fp16x6): the six terms of order <= 2^-22 (lo*hi, mid*mid, hi*lo, mid*hi, hi*mid,
+//                     hi*hi); the dropped mid*lo, lo*mid, lo*lo are <= ~2^-33 relative, below
+//                     fp32's own 2^-24 rounding of the product -- fp32-faithful products.
+template <int NPC>
+__device__ __forceinline__ floatx16 mfma_pieces(const half8 (&a)[NPC], const half8 (&b)[NPC], floatx16 c) {
+  if constexpr (NPC == 2) {
+    c = mfma16(a[1], b[0], c);
+    c = mfma16(a[0], b[1], c);
+    c = mfma16(a[0], b[0], c);
+  } else {
+    c = mfma16(a[2], b[0], c);
+    c = mfma16(a[1], b[1], c);
+    c = mfma16(a[0], b[2], c);
+    c = mfma16(a[1], b[0], c);
+    c = mfma16(a[0], b[1], c);
+    c = mfma16(a[0], b[0], c);
+  }
+  return c;
+}
+
 // Both lane halves' values of v in every lane, by one v_permlane32_swap (VALU, no LDS):
 // .x = v[lane & 31], .y = v[32 + (lane & 31)]; .x + .y == v + shfl_xor(v, 32) exactly.
 __device__ __forceinline__ float2 lane_halves(float v) {
@@ -603,20 +669,21 @@ __device__ float block_max(float v, float* red) {
   return m;
 }
 
-template <int DH, int HB, bool DIST>
+template <int DH, int HB, bool DIST, int NPC = 2>
 struct Consts16 {
   static constexpr int KS = DH / 8;                 // f16 MFMA K-steps (8 dims per lane half)
-  static constexpr int A16 = HB * KS * 2 * 64;      // uint4 entries: [hb][s][hi|lo][lane]
+  static constexpr int A16 = HB * KS * NPC * 64;    // uint4 entries: [hb][s][piece][lane]
   static constexpr int ADIST = DIST ? HB * 64 : 0;  // fp32 (S_w-scaled) distance columns
   static constexpr int EPI = 2 * 2 * HB * 16;
   static constexpr size_t BYTES = size_t(A16) * 16 + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64;
 };
 
-// ReLU as one signed-integer max on the float bits: negative floats (and -0, negative NaNs) are
-// negative int32 -> 0.0f; positive values and positive NaNs pass unchanged. One v_max_i32, no
-// canonicalising v_max_f32 on the MFMA result.
+// ReLU on the float bits that keeps every NaN, as torch.relu (model.py:71): as int32, negative
+// non-NaN floats (-0 .. -inf) are <= 0xFF800000 = -8388608 -> 0.0f; positive values (>= 0) and
+// NaNs of either sign (0xFF800001..0xFFFFFFFF = -8388607..-1) pass unchanged. v_cmp + v_cndmask;
+// a v_max_i32 alone would zero a NaN whose sign bit is set.
 __device__ __forceinline__ float relu_bits(float v) {
-  return __int_as_float(max(__float_as_int(v), 0));
+  return (__float_as_int(v) >= -8388607) ? v : 0.f;
 }
 
 template <int HB, bool REGS>
@@ -650,7 +717,7 @@ struct Epi16<HB, false> {          // b1 / w2 read from LDS: acc starts at 0, un
   }
 };
 
-template <int DH, int HB, int VAR>
+template <int DH, int HB, int VAR, int NPC>
 __global__ void __launch_bounds__(THREADS, 1)
 catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
                         const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
@@ -662,7 +729,9 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
   constexpr int D = 2 * DH;
   constexpr int KS = DH / 8;
   constexpr bool EREGS = HB <= 2 && DH <= 32;
-  using C = Consts16<DH, HB, DIST>;
+  // one-step-ahead fragment prefetch only where the registers allow it
+  constexpr bool PREF = NPC == 2 && HB <= 2;
+  using C = Consts16<DH, HB, DIST, NPC>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* A16 = reinterpret_cast<uint4*>(smem);
   float* Adist = reinterpret_cast<float*>(A16 + C::A16);
@@ -694,14 +763,16 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
   }
   const float Sw = pow2_scale(block_max(wmax, red));
   for (int f = tid; f < C::A16; f += THREADS) {
-    const int ln = f & 63, part = (f >> 6) & 1, s = ((f >> 7) % KS), hb = (f >> 7) / KS;
+    const int ln = f & 63, part = (f >> 6) % NPC, s = ((f >> 6) / NPC) % KS, hb = ((f >> 6) / NPC) / KS;
     const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 8 * s;
     half8 v;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float w = (i < p.H) ? p.w1[(int64_t)i * p.din + k0 + e] * Sw : 0.f;
       const _Float16 hi = (_Float16)w;
-      v[e] = part ? (_Float16)(w - (float)hi) : hi;
+      const float r = w - (float)hi;                  // exact
+      const _Float16 mid = (_Float16)r;
+      v[e] = part == 0 ? hi : (part == 1 ? mid : (_Float16)(r - (float)mid));
     }
     A16[f] = *reinterpret_cast<const uint4*>(&v);
   }
@@ -795,26 +866,26 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[hb][r] = epi.init(hb * 16 + r);
       float sd = 0.f;
-      uint4 an[HB][2];
+      uint4 an[HB][NPC];
+      if constexpr (PREF) {
 #pragma unroll
-      for (int hb = 0; hb < HB; ++hb) {
-        an[hb][0] = A16[((hb * KS) * 2 + 0) * 64 + lane];
-        an[hb][1] = A16[((hb * KS) * 2 + 1) * 64 + lane];
+        for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+          for (int q = 0; q < NPC; ++q) an[hb][q] = A16[((hb * KS) * NPC + q) * 64 + lane];
       }
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        uint4 ac[HB][2];
+        uint4 ac[HB][NPC];
 #pragma unroll
-        for (int hb = 0; hb < HB; ++hb) {
-          ac[hb][0] = an[hb][0];
-          ac[hb][1] = an[hb][1];
-        }
-        if (s + 1 < KS) {
+        for (int hb = 0; hb < HB; ++hb)
 #pragma unroll
-          for (int hb = 0; hb < HB; ++hb) {
-            an[hb][0] = A16[((hb * KS + s + 1) * 2 + 0) * 64 + lane];
-            an[hb][1] = A16[((hb * KS + s + 1) * 2 + 1) * 64 + lane];
-          }
+          for (int q = 0; q < NPC; ++q)
+            ac[hb][q] = PREF ? an[hb][q] : A16[((hb * KS + s) * NPC + q) * 64 + lane];
+        if (PREF && s + 1 < KS) {
+#pragma unroll
+          for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+            for (int q = 0; q < NPC; ++q) an[hb][q] = A16[((hb * KS + s + 1) * NPC + q) * 64 + lane];
         }
         const float4 h0 = *reinterpret_cast<const float4*>(hr + 8 * s);
         const float4 h1 = *reinterpret_cast<const float4*>(hr + 8 * s + 4);
@@ -829,15 +900,14 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
         x[7] = tv[8 * s + 7] * h1.w;
 #pragma unroll
         for (int e = 0; e < 8; ++e) sd += x[e];
-        half8 xh, xl;
-        split8(x, xh, xl);
+        half8 xp[NPC];
+        split_pieces<NPC>(x, xp);
 #pragma unroll
         for (int hb = 0; hb < HB; ++hb) {
-          const half8 ah = *reinterpret_cast<const half8*>(&ac[hb][0]);
-          const half8 al = *reinterpret_cast<const half8*>(&ac[hb][1]);
-          acc[hb] = mfma16(al, xh, acc[hb]);
-          acc[hb] = mfma16(ah, xl, acc[hb]);
-          acc[hb] = mfma16(ah, xh, acc[hb]);
+          half8 ap_[NPC];
+#pragma unroll
+          for (int q = 0; q < NPC; ++q) ap_[q] = *reinterpret_cast<const half8*>(&ac[hb][q]);
+          acc[hb] = mfma_pieces<NPC>(ap_, xp, acc[hb]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -899,18 +969,19 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // candidate into B fragments that stay in VGPRs for the whole sweep. The per-(c, j) VALU work
 // is then only the epilogue and h_j . t_c -- no per-pair conversions.
 // ---------------------------------------------------------------------------------------------
-template <int DH, int HB, bool DIST, int NW = WAVES>
+template <int DH, int HB, bool DIST, int NW = WAVES, int NPC = 2>
 struct CfgB {
   static constexpr int D = 2 * DH;
   static constexpr int KS = DH / 8;
-  static constexpr int NE = HB * KS * 64;             // uint4 fragment entries per item (hi or lo)
-  static constexpr int IB = NE * 16 * 2;              // bytes per item (hi + lo)
+  static constexpr int NE = HB * KS * 64;             // uint4 fragment entries per item and piece
+  static constexpr int IB = NE * 16 * NPC;            // bytes per item (all pieces)
 #ifdef NAIS_X3B_G
   static constexpr int G = NAIS_X3B_G;
 #else
   static constexpr int G = IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1);   // items per ring group
 #endif
-  static constexpr int JCB = (2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;  // LDS chunk rows
+  // LDS chunk rows; fp16x6 keeps 32 (the s tile below) even where 64 would fit
+  static constexpr int JCB = (NPC == 3 || 2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;
   static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);  // build entries per thread
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
@@ -920,14 +991,14 @@ struct CfgB {
 #ifdef NAIS_X3B_NOPIPE
   static constexpr bool PIPE = false;   // debug: the wide epilogue structure for every shape
 #else
-  static constexpr bool PIPE = HB <= 2 && DH <= 32;
+  static constexpr bool PIPE = NPC == 2 && HB <= 2 && DH <= 32;
 #endif
   static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
                                   size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
 };
 
 // NW = waves per workgroup (2 per SIMD at 8). D, H <= 64 pipeline the epilogue (CfgB::PIPE).
-template <int DH, int HB, int VAR, int NW>
+template <int DH, int HB, int VAR, int NW, int NPC>
 __global__ void __launch_bounds__(NW * 64, 1)
 catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
@@ -936,7 +1007,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
   constexpr bool REGION = VarT<VAR>::REGION;
   constexpr bool DIST = VarT<VAR>::DIST;
-  using C = CfgB<DH, HB, DIST, NW>;
+  using C = CfgB<DH, HB, DIST, NW, NPC>;
   constexpr int D = C::D, KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT;
   constexpr int THREADS = NW * 64, CAND_PER_BLOCK = NW * 32;   // shadow the 8-wave defaults
   constexpr bool PIPE = C::PIPE;
@@ -947,8 +1018,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #endif
   constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][hi|lo][NE]
-  float* Adist = reinterpret_cast<float*>(ring + 2 * G * 2 * NE);
+  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][piece][NE]
+  float* Adist = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);
   float* Eimg = Adist + C::ADIST;
   float* red = Eimg + C::EPI;
   float* hrows = red + 16;
@@ -1017,7 +1088,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
   const float St = pow2_scale(tmax);
   const float invSt = 1.f / St;
-  half8 tb_hi[KS], tb_lo[KS];
+  half8 tb[KS][NPC];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     float x[8];
@@ -1026,7 +1097,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       tv[8 * s + e] *= St;
       x[e] = tv[8 * s + e];
     }
-    split8(x, tb_hi[s], tb_lo[s]);
+    split_pieces<NPC>(x, tb[s]);
   }
   double clat = 0.0, clon = 0.0;
   DistW dw{0.f, 0.f, 0.f};
@@ -1050,7 +1121,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
   auto build = [&](int jj, int grp, int it) {
     const float* hr = hrows + jj * D;
-    uint4* dst = ring + ((grp * G + it) * 2) * NE;
+    uint4* dst = ring + ((grp * G + it) * NPC) * NE;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * THREADS;
@@ -1068,10 +1139,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         a[5] = wv[q][5] * h1.y;
         a[6] = wv[q][6] * h1.z;
         a[7] = wv[q][7] * h1.w;
-        half8 hi, lo;
-        split8(a, hi, lo);
-        dst[e] = *reinterpret_cast<const uint4*>(&hi);
-        dst[NE + e] = *reinterpret_cast<const uint4*>(&lo);
+        half8 pc[NPC];
+        split_pieces<NPC>(a, pc);
+#pragma unroll
+        for (int q2 = 0; q2 < NPC; ++q2) dst[q2 * NE + e] = *reinterpret_cast<const uint4*>(&pc[q2]);
       }
     }
   };
@@ -1137,13 +1208,13 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       if (MMA) {
 #pragma unroll
         for (int hb = 0; hb < HB; ++hb) {
-          const uint4 ahu = src[(hb * KS + s) * 64 + lane];
-          const uint4 alu = src[NE + (hb * KS + s) * 64 + lane];
-          const half8 ah = *reinterpret_cast<const half8*>(&ahu);
-          const half8 al = *reinterpret_cast<const half8*>(&alu);
-          accN[hb] = mfma16(al, tb_hi[s], accN[hb]);
-          accN[hb] = mfma16(ah, tb_lo[s], accN[hb]);
-          accN[hb] = mfma16(ah, tb_hi[s], accN[hb]);
+          half8 ap_[NPC];
+#pragma unroll
+          for (int q = 0; q < NPC; ++q) {
+            const uint4 u4 = src[q * NE + (hb * KS + s) * 64 + lane];
+            ap_[q] = *reinterpret_cast<const half8*>(&u4);
+          }
+          accN[hb] = mfma_pieces<NPC>(ap_, tb[s], accN[hb]);
         }
       }
       if constexpr (EPIL) {
@@ -1195,13 +1266,13 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       for (int s = 0; s < KS; ++s) {
 #pragma unroll
         for (int hb = 0; hb < HS; ++hb) {
-          const uint4 ahu = src[((h0 + hb) * KS + s) * 64 + lane];
-          const uint4 alu = src[NE + ((h0 + hb) * KS + s) * 64 + lane];
-          const half8 ah = *reinterpret_cast<const half8*>(&ahu);
-          const half8 al = *reinterpret_cast<const half8*>(&alu);
-          acc[hb] = mfma16(al, tb_hi[s], acc[hb]);
-          acc[hb] = mfma16(ah, tb_lo[s], acc[hb]);
-          acc[hb] = mfma16(ah, tb_hi[s], acc[hb]);
+          half8 ap_[NPC];
+#pragma unroll
+          for (int q = 0; q < NPC; ++q) {
+            const uint4 u4 = src[q * NE + ((h0 + hb) * KS + s) * 64 + lane];
+            ap_[q] = *reinterpret_cast<const half8*>(&u4);
+          }
+          acc[hb] = mfma_pieces<NPC>(ap_, tb[s], acc[hb]);
         }
       }
 #pragma unroll
@@ -1269,11 +1340,9 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         x[2] = ok ? h0.z * Sh : 0.f; x[3] = ok ? h0.w * Sh : 0.f;
         x[4] = ok ? h1.x * Sh : 0.f; x[5] = ok ? h1.y * Sh : 0.f;
         x[6] = ok ? h1.z * Sh : 0.f; x[7] = ok ? h1.w * Sh : 0.f;
-        half8 ah, al;
-        split8(x, ah, al);
-        sacc = mfma16(al, tb_hi[s], sacc);
-        sacc = mfma16(ah, tb_lo[s], sacc);
-        sacc = mfma16(ah, tb_hi[s], sacc);
+        half8 hpc[NPC];
+        split_pieces<NPC>(x, hpc);
+        sacc = mfma_pieces<NPC>(hpc, tb[s], sacc);
       }
     }
 #pragma unroll
@@ -1303,7 +1372,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
         const int jj = g * G + it;
         if (jj < jn) {
           floatx16 accN[HB];
-          const uint4* src = ring + (((g & 1) * G + it) * 2) * NE;
+          const uint4* src = ring + (((g & 1) * G + it) * NPC) * NE;
           if constexpr (PIPE) {
             step(std::true_type{}, std::true_type{}, src, accN, accP, jj, prev, prev >= 0);
 #pragma unroll
@@ -1837,8 +1906,7 @@ struct Shape {
 int validate(const nais_params_t* p, Shape* sh) {
   if (!p) return fail(NAIS_E_INVALID, "params is NULL");
   if (p->variant < 0 || p->variant > 3) return fail(NAIS_E_INVALID, "unknown variant");
-  if (p->precision != NAIS_PRECISION_FP32 && p->precision != NAIS_PRECISION_FP16X3 &&
-      p->precision != NAIS_PRECISION_FP16X3_PAIRSPLIT)
+  if (p->precision < NAIS_PRECISION_FP32 || p->precision > NAIS_PRECISION_FP16X6_PAIRSPLIT)
     return fail(NAIS_E_INVALID, "unknown precision");
   if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
     return fail(NAIS_E_INVALID, "missing parameter pointer");
@@ -1916,14 +1984,14 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
   return check_launch("catalog_score_kernel");
 }
 
-template <int DH, int HB, int VAR>
+template <int DH, int HB, int VAR, int NPC>
 size_t catalog_x3_lds() {
   constexpr bool DIST = VarT<VAR>::DIST;
-  return Consts16<DH, HB, DIST>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
+  return Consts16<DH, HB, DIST, NPC>::BYTES + size_t(JC) * 2 * DH * 4 + size_t(JC) * 4 +
          (DIST ? size_t(JC) * 16 : 0);
 }
 
-template <int DH, int HB, int VAR>
+template <int DH, int HB, int VAR, int NPC = 2>
 int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                       const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                       const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
@@ -1932,8 +2000,8 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
   } else {
-    const size_t lds = catalog_x3_lds<DH, HB, VAR>();
-    auto kern = catalog_score_x3_kernel<DH, HB, VAR>;
+    const size_t lds = catalog_x3_lds<DH, HB, VAR, NPC>();
+    auto kern = catalog_score_x3_kernel<DH, HB, VAR, NPC>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1947,7 +2015,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
   }
 }
 
-template <int DH, int HB, int VAR>
+template <int DH, int HB, int VAR, int NPC = 2>
 int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                        const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                        const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
@@ -1957,12 +2025,12 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                                        scores, ld, nan_count, stream, tab);
   } else if constexpr (VarT<VAR>::DIST || (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32))) {
     // the distance features ride on the per-pair split kernel (also in pair-table mode)
-    return launch_catalog_x3<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords,
-                                          latlon_mat, scores, ld, nan_count, stream, tab);
+    return launch_catalog_x3<DH, HB, VAR, NPC>(d, indptr, indices, users, nb, region_of, coords,
+                                               latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
     constexpr int NW = WAVES;
-    const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW>::BYTES;
-    auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW>;
+    const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW, NPC>::BYTES;
+    auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW, NPC>;
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1974,6 +2042,23 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                        coords, latlon_mat, scores, ld, nan_count, tab);
     return check_launch("catalog_score_x3b_kernel");
   }
+}
+
+template <int DH, int HB, int VAR>
+int launch_catalog_x6b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
+                       const int32_t* users, int nb, const int64_t* region_of, const double* coords,
+                       const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
+                       hipStream_t stream, const TableOut& tab = TableOut{}) {
+  return launch_catalog_x3b<DH, HB, VAR, 3>(d, indptr, indices, users, nb, region_of, coords,
+                                            latlon_mat, scores, ld, nan_count, stream, tab);
+}
+template <int DH, int HB, int VAR>
+int launch_catalog_x6(const DevParams& d, const int64_t* indptr, const int64_t* indices,
+                      const int32_t* users, int nb, const int64_t* region_of, const double* coords,
+                      const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
+                      hipStream_t stream, const TableOut& tab = TableOut{}) {
+  return launch_catalog_x3<DH, HB, VAR, 3>(d, indptr, indices, users, nb, region_of, coords,
+                                           latlon_mat, scores, ld, nan_count, stream, tab);
 }
 
 template <int DH, int HB, int VAR>
@@ -2117,7 +2202,13 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
   const int64_t ld = round_up(params->num_pois, 64);
   for (int32_t u0 = 0; u0 < num_users; u0 += MAX_BATCH_USERS) {
     const int nb = std::min<int32_t>(MAX_BATCH_USERS, num_users - u0);
-    if (params->precision == NAIS_PRECISION_FP16X3)
+    if (params->precision == NAIS_PRECISION_FP16X6)
+      NAIS_DISPATCH(launch_catalog_x6b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X6_PAIRSPLIT)
+      NAIS_DISPATCH(launch_catalog_x6, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X3)
       NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
                     nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
     else if (params->precision == NAIS_PRECISION_FP16X3_PAIRSPLIT)
@@ -2187,6 +2278,10 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
     if (params->precision == NAIS_PRECISION_FP32)
       NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, nullptr, items + base, nullptr,
                     ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
+    else if (params->precision == NAIS_PRECISION_FP16X6 ||
+             params->precision == NAIS_PRECISION_FP16X6_PAIRSPLIT)
+      NAIS_DISPATCH(launch_catalog_x6b, sh.DH, sh.HB, params->variant, d, nullptr, items + base,
+                    nullptr, ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
     else
       NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, nullptr, items + base,
                     nullptr, ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
@@ -2219,7 +2314,15 @@ int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,
   if (rc) return rc;
   for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
     const int nb = std::min<int32_t>(65535, num_users - u0);
-    if (params->precision == NAIS_PRECISION_FP16X3)
+    if (params->precision == NAIS_PRECISION_FP16X6)
+      NAIS_DISPATCH(launch_catalog_x6b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                    nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X6_PAIRSPLIT)
+      NAIS_DISPATCH(launch_catalog_x6, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
+                    nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
+                    nan_count, st);
+    else if (params->precision == NAIS_PRECISION_FP16X3)
       NAIS_DISPATCH(launch_catalog_x3b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
                     nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
                     nan_count, st);

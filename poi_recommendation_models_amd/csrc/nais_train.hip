@@ -249,7 +249,7 @@ __device__ __forceinline__ void pair_forward(const TrainArgs& ar, const float* L
       float v = acc[hb][r];
       if (ar.drop.on) v *= ar.drop.factor(k, i);
       acc[hb][r] = v;
-      ap = fmaf(L[T::O_W2 + i], fmaxf(v, 0.f), ap);
+      ap = fmaf(L[T::O_W2 + i], nais_relu(v), ap);
     }
   }
   a = ap + __shfl_xor(ap, 32);
@@ -457,7 +457,7 @@ train_backward_kernel(TrainArgs a, const float* __restrict__ saved, const float*
         const int i = crow(hb, r, hh);
         const float v = acc[hb][r];
         const float wi = L[T::O_W2 + i];
-        gw2[hb * 16 + r] = fmaf(da, fmaxf(v, 0.f), gw2[hb * 16 + r]);
+        gw2[hb * 16 + r] = fmaf(da, nais_relu(v), gw2[hb * 16 + r]);
         const float du = v > 0.f ? da * wi * sc : 0.f;
         gb1[hb * 16 + r] += du;
         acc[hb][r] = du;
@@ -996,7 +996,7 @@ __device__ __forceinline__ void gm_pair_forward(const GArgs& a, const GL& g, con
       float v = acc[hb][r];
       if (a.drop.on) v *= a.drop.factor(key, i);
       acc[hb][r] = v;
-      ap = fmaf(L[g.o_w2 + i], fmaxf(v, 0.f), ap);
+      ap = fmaf(L[g.o_w2 + i], nais_relu(v), ap);
     }
   }
   alogit = ap + __shfl_xor(ap, 32);
@@ -1087,7 +1087,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       const float du = v > 0.f ? da * L[g.o_w2 + i] * m : 0.f;   // ReLU + dropout backward
       acc[hb][r] = du;
       vb[r] = du;
-      vz[r] = da * fmaxf(v, 0.f);
+      vz[r] = da * nais_relu(v);
     }
     const float tb = half_reduce_scatter<16>(vb, lane);
     const float tz = half_reduce_scatter<16>(vz, lane);

@@ -61,12 +61,14 @@ class _NAISDevice(nn.Module):
     VARIANT = _capi.VARIANT_BASIC
     report_nan = True  # model.py:50-54 prints the NaN count of every forward
     # arithmetic of the catalog scorer's W1 x products (include/nais.h NAIS_PRECISION_*):
-    #   "fp16x3" (default) split-fp16 MFMA, 3 products per fp32 product, fp32 accumulation,
-    #            ~2^-21 relative per product -- 2.6x the fp32 path, same max |dscore| vs the
-    #            reference on every golden set (tests/test_gpu_parity.py);
-    #   "fp32"   exact fp32 MFMA (a k-ordered fmaf chain); "fp16x3_pairsplit" alternative split.
+    #   "fp16x6" (default) fp32-faithful split-fp16 MFMA: hi/mid/lo pieces represent every fp32
+    #            operand exactly, 6 products per fp32 product (dropped terms <= ~2^-33 relative,
+    #            below fp32's own product rounding), fp32 accumulation;
+    #   "fp32"   exact fp32 MFMA (a k-ordered fmaf chain);
+    #   "fp16x3" 2 pieces / 3 products (~2^-21 relative per product: narrower than fp32, kept for
+    #            A/B); "*_pairsplit" split x = h (.) t per pair instead of A_j = W1 diag(h_j).
     # nais_forward (the general model.forward path) is always fp32.
-    precision = "fp16x3"
+    precision = "fp16x6"
     # full-catalog strategy of catalog.score_topk / the validation drop-ins: "auto" (pair tables
     # when the users' history entries outnumber their distinct POIs 3:1, else per user),
     # "direct" or "pairs" (include/nais.h)
@@ -114,7 +116,9 @@ class _NAISDevice(nn.Module):
         p.num_regions = self.embed_region.weight.shape[0] if hasattr(self, "embed_region") else 0
         p.beta = float(self.beta)
         p.precision = {"fp32": _capi.PRECISION_FP32, "fp16x3": _capi.PRECISION_FP16X3,
-                       "fp16x3_pairsplit": _capi.PRECISION_FP16X3_PAIRSPLIT}[self.precision]
+                       "fp16x3_pairsplit": _capi.PRECISION_FP16X3_PAIRSPLIT,
+                       "fp16x6": _capi.PRECISION_FP16X6,
+                       "fp16x6_pairsplit": _capi.PRECISION_FP16X6_PAIRSPLIT}[self.precision]
         p.embed_history = eh.data_ptr()
         p.embed_target = et.data_ptr()
         p.embed_region = self.embed_region.weight.data_ptr() if hasattr(self, "embed_region") else None

@@ -76,11 +76,39 @@ def gather_topk(local_users, local_ids, local_scores, num_users, group=None):
     return ids, sc
 
 
+def column_blocks(num_pois, world):
+    """[(c0, c1)] per rank: rank r owns POIs [r*S, (r+1)*S) clipped to P, S = ceil(P / world).
+    With P % world != 0 the last block is narrower, and a rank may own no column at all."""
+    S = (num_pois + world - 1) // world
+    return [(min(r * S, num_pois), min((r + 1) * S, num_pois)) for r in range(world)]
+
+
+def min_block_candidates(csr, users, num_pois, world):
+    """min over (listed user, rank) of the candidates the user has inside the rank's column block:
+    the block's width minus the user's history POIs that fall in it. The column-sharded merge
+    needs >= k of them everywhere (a short block list would be padded with id -1)."""
+    users = np.asarray(list(users), dtype=np.int64)
+    if len(users) == 0:
+        return num_pois
+    blocks = column_blocks(num_pois, world)
+    width = np.array([c1 - c0 for c0, c1 in blocks], dtype=np.int64)
+    S = (num_pois + world - 1) // world
+    h = csr.hist_len[users]
+    rows = np.repeat(np.arange(len(users)), h)
+    starts = csr.host_indptr[users]
+    pos = np.repeat(starts - np.concatenate([[0], np.cumsum(h)[:-1]]), h) + np.arange(int(h.sum()))
+    blk = csr.host_indices[pos] // S
+    inside = np.zeros((len(users), world), dtype=np.int64)
+    np.add.at(inside, (rows, blk), 1)
+    return int((width[None, :] - inside).min())
+
+
 def distributed_plan(csr, num_users, num_pois, k, world, model=None):
     """"pairs" (column-sharded, distributed_topk_pairs) when the users' histories share POIs
-    (entries >= catalog.PAIR_MIN_SHARING x distinct POIs) and every column block keeps k candidates
-    per user; else "users" (LPT user sharding with replicated tables). With user sharding and
-    shared histories every rank would build the full pair tables; column sharding splits them."""
+    (entries >= catalog.PAIR_MIN_SHARING x distinct POIs) and every rank's column block keeps k
+    candidates for every user; else "users" (LPT user sharding with replicated tables). With user
+    sharding and shared histories every rank would build the full pair tables; column sharding
+    splits them."""
     from . import catalog
     if world < 2 or (model is not None and model._pairs_only):
         return "pairs" if model is not None and model._pairs_only else "users"
@@ -88,8 +116,8 @@ def distributed_plan(csr, num_users, num_pois, k, world, model=None):
     entries = int(hist.sum())
     used = csr.host_indices[:int(csr.host_indptr[num_users])]
     distinct = int(np.count_nonzero(np.bincount(used, minlength=num_pois))) if entries else 0
-    S = (num_pois + world - 1) // world
-    if distinct and entries >= catalog.PAIR_MIN_SHARING * distinct and S - int(hist.max(initial=0)) >= k:
+    if (distinct and entries >= catalog.PAIR_MIN_SHARING * distinct
+            and min_block_candidates(csr, range(num_users), num_pois, world) >= k):
         return "pairs"
     return "users"
 
@@ -143,10 +171,10 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     P = csr.shape[1]
     users = np.asarray(list(users), dtype=np.int64)
     n = len(users)
-    S = (P + world - 1) // world
-    if world > 1 and S - int(csr.hist_len[users].max(initial=0)) < k:
-        raise ValueError("a column block has fewer than k candidates for some user")
-    c0, c1 = min(rank * S, P), min((rank + 1) * S, P)
+    if world > 1 and min_block_candidates(csr, users, P, world) < k:
+        raise ValueError("a column block has fewer than k candidates for some user "
+                         "(use the user-sharded path, distributed_topk falls back to it)")
+    c0, c1 = column_blocks(P, world)[rank]
     ids, sc = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
                                 kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events)
     if world == 1:

@@ -5,6 +5,12 @@ device with the fused NAIS kernel + radix-select top-k (`catalog.score_topk`), b
 `recommended_list` (args.topk POI ids per user, best first) and returns
 (precision_v, recall_v, hit_v, precision_t, recall_t, hit_t) from `eval_metrics.evaluate_mp`.
 The model must be one of this package's NAIS modules, on a ROCm device.
+
+Multi-GPU: when a torch.distributed process group with more than one rank is initialised (one
+process per GPU, as torchrun starts them), every function here evaluates cooperatively across the
+ranks (sharding.distributed_topk: column-sharded pairs route or LPT user sharding) and returns the
+same 6-tuple on every rank, so run.py's call sites (run.py:112-116, 178-182, 259-263) stay as they
+are. Every rank must make the call.
 """
 from __future__ import annotations
 
@@ -12,9 +18,23 @@ from . import eval_metrics
 from .catalog import score_topk
 
 
+def _distributed_world():
+    try:
+        import torch.distributed as dist
+    except Exception:
+        return 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size()
+
+
 def _recommend_ids(model, args, num_users, train_matrix, **kw):
     model.eval()                                               # validation.py:8
-    ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
+    if _distributed_world() > 1:
+        from .sharding import distributed_topk
+        ids, _ = distributed_topk(model, train_matrix, num_users, args.topk, **kw)
+    else:
+        ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
     nan = int(model._last_nan.item())
     if nan > 0 and type(model).__name__ == "NAIS_basic" and model.report_nan:
         print(nan)                                             # model.py:53-54

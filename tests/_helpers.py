@@ -30,26 +30,43 @@ def positives_from(z, kind):
     return out
 
 
-def tie_groups(scores, tie_eps):
-    """Split a descending score list into maximal runs whose neighbours differ by <= tie_eps."""
+def ulp32(x):
+    """fp32 unit in the last place of |x| (elementwise)."""
+    a = np.abs(np.asarray(x, dtype=np.float32))
+    return np.spacing(a).astype(np.float64)
+
+
+def tie_groups(scores, tie_eps=0.0, tie_ulps=None):
+    """Split a descending score list into maximal runs whose neighbours differ by <= tie_eps
+    (absolute) or, with `tie_ulps`, by <= tie_ulps fp32 ulps of the larger neighbour."""
     groups, start = [], 0
     for i in range(1, len(scores) + 1):
-        if i == len(scores) or (scores[i - 1] - scores[i]) > tie_eps or np.isnan(scores[i]) != np.isnan(scores[i - 1]):
+        if i < len(scores):
+            gap = scores[i - 1] - scores[i]
+            eps = tie_eps if tie_ulps is None else tie_ulps * float(ulp32(max(abs(scores[i - 1]),
+                                                                             abs(scores[i]))))
+        if i == len(scores) or gap > eps or np.isnan(scores[i]) != np.isnan(scores[i - 1]):
             groups.append((start, i))
             start = i
     return groups
 
 
-def assert_topk_equivalent(ref_ids, ref_scores, our_ids, our_scores, tie_eps,
-                           score_atol=SCORE_ATOL, lookup=None):
+# per-call statistics of assert_topk_equivalent: lists checked, tie runs compared as sets, and
+# how many of those runs are not exact fp32 ties (they rely on the ulp allowance)
+TIE_STATS = {"lists": 0, "set_runs": 0, "inexact_runs": 0}
+
+
+def assert_topk_equivalent(ref_ids, ref_scores, our_ids, our_scores, tie_eps=0.0,
+                           score_atol=SCORE_ATOL, lookup=None, tie_ulps=None):
     """Tie-aware top-k parity (SURVEY.md 8(a) 'Tie rule').
 
-    Wherever the reference's sorted scores are separated by more than `tie_eps`, the id at
-    each position must be identical. Inside a run of scores within `tie_eps` of each other the
-    ids are compared as a set; for the run that straddles rank k, each of our ids that the
-    reference did not list must carry a score within `tie_eps` of that run (its reference score
-    when `lookup` (id -> reference score) is given, else our own). Scores at equal positions
-    must agree within `score_atol`.
+    Wherever the reference's sorted scores are separated by more than `tie_eps` (or, with
+    `tie_ulps`, by more than that many fp32 ulps), the id at each position must be identical.
+    Inside a run of scores within that distance of each other the ids are compared as a set; for
+    the run that straddles rank k, each of our ids that the reference did not list must carry a
+    score within the tie distance of that run (its reference score when `lookup` (id -> reference
+    score) is given, else our own). Scores at equal positions must agree within `score_atol`.
+    Returns the number of tie runs compared as sets (TIE_STATS accumulates them).
     """
     ref_ids = [int(x) for x in ref_ids]
     our_ids = [int(x) for x in our_ids]
@@ -62,17 +79,26 @@ def assert_topk_equivalent(ref_ids, ref_scores, our_ids, our_scores, tie_eps,
     assert np.array_equal(np.isnan(ref_scores), np.isnan(our_scores))
     assert np.all(np.abs(ref_scores[both] - our_scores[both]) <= score_atol), \
         np.max(np.abs(ref_scores[both] - our_scores[both]))
-    groups = tie_groups(ref_scores, tie_eps)
+    groups = tie_groups(ref_scores, tie_eps, tie_ulps)
+    runs = 0
+    TIE_STATS["lists"] += 1
     for gi, (a, b) in enumerate(groups):
+        if b - a > 1:
+            runs += 1
+            TIE_STATS["set_runs"] += 1
+            if not np.all(ref_scores[a:b] == ref_scores[a]):
+                TIE_STATS["inexact_runs"] += 1
         r, o = set(ref_ids[a:b]), set(our_ids[a:b])
         if gi < len(groups) - 1:
             assert r == o, f"positions {a}:{b}: ref {sorted(r)} ours {sorted(o)}"
         else:
-            lo = ref_scores[b - 1] - tie_eps
-            hi = ref_scores[a] + tie_eps
+            eps = tie_eps if tie_ulps is None else tie_ulps * float(ulp32(ref_scores[a]))
+            lo = ref_scores[b - 1] - eps
+            hi = ref_scores[a] + eps
             for pos in range(a, b):
                 c = our_ids[pos]
                 if c in r:
                     continue
                 s = lookup[c] if lookup is not None and c in lookup else our_scores[pos]
                 assert lo <= s <= hi, f"id {c} at pos {pos} score {s} outside tie run [{lo},{hi}]"
+    return runs

@@ -1,0 +1,164 @@
+"""GPU parity at the BASELINE.json configurations, through the C-ABI.
+
+* config 4 -- the benchmarked path itself: the bench's whole job (50k users x 100k POIs,
+  d = H = 64, h ~ U{1..200}, the bench's seeds) through catalog._score_topk_pairs with the bench's
+  default knobs (fp16x6 tables, CU-masked overlap, 512-column blocks, fused running top-k,
+  longest-first order). Every user's top-50 against the per-user ("direct") kernels, 4 users
+  against the numpy oracle.
+* config 2 -- P = 50k, d = H = 64, h <= 100: a 600-user slice through both routes vs each other
+  and vs the oracle.
+* config 5 -- P = 1M, d = H = 128, h <= 200: 8 users through the direct route (full rows + top-50)
+  and a forced pairs route over one column block, against the oracle (sampled candidates + the
+  winners for every user, the full row for one user).
+
+Tie rule: tests/_helpers.assert_topk_equivalent with 4 fp32 ulps; every test
+prints how many tie runs were compared as sets and how many of them are not exact fp32 ties.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _helpers import SCORE_ATOL, TIE_STATS, assert_topk_equivalent
+from oracle import nais_oracle
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TIE_ULPS = 4
+
+
+def _model(p, P, D, H):
+    from poi_recommendation_models_amd.model import NAIS_basic
+    m = NAIS_basic(P, D, H, 0.5)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()}, strict=False)
+    m.report_nan = False
+    return m.to(DEV).eval()
+
+
+def _compare_lists(ids_a, sc_a, ids_b, sc_b, users):
+    """Tie-aware comparison of two [n, k] top-k sets (a = reference side); rows whose ids are
+    identical and scores within SCORE_ATOL are accepted vectorised, the rest one by one."""
+    same = np.all(ids_a == ids_b, axis=1) & np.all(np.abs(sc_a - sc_b) <= SCORE_ATOL, axis=1)
+    runs = 0
+    for r in np.nonzero(~same)[0]:
+        runs += assert_topk_equivalent(ids_a[r], sc_a[r], ids_b[r], sc_b[r], tie_ulps=TIE_ULPS)
+    return int((~same).sum()), runs
+
+
+def _stats(tag, before):
+    d = {k: TIE_STATS[k] - before[k] for k in TIE_STATS}
+    print(f"{tag}: tie runs compared as sets {d['set_runs']} over {d['lists']} lists, "
+          f"{d['inexact_runs']} of them not exact fp32 ties")
+
+
+def test_config4_bench_job_pairs_vs_direct_and_oracle():
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs, score_topk
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    before = dict(TIE_STATS)
+    U, P, D, H, K = 50_000, 100_000, 64, 64, 50
+    data = make_checkins(U, P, 200, seed=2024)                   # bench.py's workload
+    p = init_nais_params(P, D, H, seed=7, emb_std=0.3, bias_std=0.1)
+    m = _model(p, P, D, H)
+    assert m.precision == "fp16x6"
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    users = np.arange(U)
+    ev = []
+    ids, sc = _score_topk_pairs(m, csr, users, K, None, None, None, None, force=True, events=ev)
+    settings = {k: n for k, a, b, n in ev if a is None}
+    assert settings["table_cus"] not in (0, torch.cuda.get_device_properties(DEV).multi_processor_count)
+    assert catalog.PAIR_FUSED_TOPK and catalog.PAIR_LPT_ORDER and catalog.PAIR_BLOCK_COLS == 512
+    ids_p, sc_p = ids.cpu().numpy(), sc.cpu().numpy()
+    ids_d, sc_d = score_topk(m, csr, users, K, strategy="direct")
+    ids_d, sc_d = ids_d.cpu().numpy(), sc_d.cpu().numpy()
+    hist_ok = all(not np.isin(ids_p[u], data.history(u)).any() for u in range(0, U, 97))
+    assert hist_ok
+    assert not np.isnan(sc_p).any()
+    nd, runs = _compare_lists(ids_d, sc_d, ids_p, sc_p, users)
+    print(f"config 4: {U} users, {nd} lists differ from the direct route in some position "
+          f"(resolved by the tie rule, {runs} tie runs), max |score| diff at equal positions "
+          f"{np.max(np.abs(sc_p - sc_d)):.3g}")
+    # 4 users against the numpy oracle: the shortest, the longest and two others
+    h = data.hist_len()
+    for u in (int(np.argmin(h)), int(np.argmax(h)), 1, 4242):
+        cand, ref = nais_oracle.catalog_scores_basic(p, data.history(u), P, chunk=4096)
+        rid, rsc = nais_oracle.topk_ids(cand, ref, K)
+        lookup = dict(zip(cand.tolist(), ref.tolist()))
+        assert_topk_equivalent(rid, rsc, ids_p[u], sc_p[u], tie_ulps=TIE_ULPS, lookup=lookup)
+        got = np.array([lookup[int(c)] for c in ids_p[u]])
+        assert np.max(np.abs(got - sc_p[u])) <= SCORE_ATOL
+        print(f"  user {u} (h={h[u]}): max |score - oracle| over its top-50 "
+              f"{np.max(np.abs(got - sc_p[u])):.3g}")
+    _stats("config 4", before)
+
+
+def test_config2_slice_both_routes():
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    before = dict(TIE_STATS)
+    U, P, D, H, K = 600, 50_000, 64, 64, 50
+    data = make_checkins(U, P, 100, seed=202)
+    p = init_nais_params(P, D, H, seed=203, emb_std=0.3, bias_std=0.1)
+    m = _model(p, P, D, H)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    users = np.arange(U)
+    ia, sa = score_topk(m, csr, users, K, strategy="direct")
+    ib, sb = score_topk(m, csr, users, K, strategy="pairs")
+    ia, sa, ib, sb = (x.cpu().numpy() for x in (ia, sa, ib, sb))
+    nd, _ = _compare_lists(ia, sa, ib, sb, users)
+    print(f"config 2 slice: {nd} of {U} lists differ between the routes (tie rule)")
+    for u in (0, 1, 2):
+        cand, ref = nais_oracle.catalog_scores_basic(p, data.history(u), P, chunk=4096)
+        rid, rsc = nais_oracle.topk_ids(cand, ref, K)
+        lookup = dict(zip(cand.tolist(), ref.tolist()))
+        for ids, sc in ((ia, sa), (ib, sb)):
+            assert_topk_equivalent(rid, rsc, ids[u], sc[u], tie_ulps=TIE_ULPS, lookup=lookup)
+    _stats("config 2", before)
+
+
+def test_config5_slice_direct_and_pairs_block():
+    from poi_recommendation_models_amd.catalog import (DeviceCSR, _score_topk_pairs, score_catalog,
+                                                       score_topk)
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    before = dict(TIE_STATS)
+    U, P, D, H, K = 8, 1_000_000, 128, 128, 50
+    data = make_checkins(U, P, 200, seed=505)
+    p = init_nais_params(P, D, H, seed=506, emb_std=0.3, bias_std=0.1)
+    m = _model(p, P, D, H)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    users = np.arange(U)
+    full = score_catalog(m, csr, users).cpu().numpy()            # direct route, fp16x6
+    ids, sc = score_topk(m, csr, users, K, strategy="direct")
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    rng = np.random.default_rng(7)
+    h = data.hist_len()
+    for u in range(U):
+        hist = data.history(u)
+        assert np.all(full[u][hist] == -1.0)
+        cand = nais_oracle.complement_candidates(hist, P)
+        oid, osc = nais_oracle.topk_ids(cand, full[u][cand], K)   # top-k == our own full row's
+        np.testing.assert_array_equal(ids[u], oid)
+        np.testing.assert_array_equal(sc[u], osc)
+        probe = np.unique(np.concatenate([ids[u], rng.choice(cand, 1500, replace=False)]))
+        ref, _ = nais_oracle.forward_basic(p, np.broadcast_to(hist, (len(probe), len(hist))), probe)
+        assert np.max(np.abs(full[u][probe] - ref)) <= SCORE_ATOL, (u, np.max(np.abs(full[u][probe] - ref)))
+    # one full oracle row (the shortest history) -> tie-aware top-50 against the reference order
+    u = int(np.argmin(h))
+    cand, ref = nais_oracle.catalog_scores_basic(p, data.history(u), P, chunk=8192)
+    rid, rsc = nais_oracle.topk_ids(cand, ref, K)
+    assert_topk_equivalent(rid, rsc, ids[u], sc[u], tie_ulps=TIE_ULPS,
+                           lookup=dict(zip(cand.tolist(), ref.tolist())))
+    assert np.max(np.abs(full[u][cand] - ref)) <= SCORE_ATOL
+    # the pairs route forced over one 4,096-column block of the catalog
+    c0, c1 = 400_000, 404_096
+    pid, psc = _score_topk_pairs(m, csr, users, K, None, None, None, None, force=True, cols=(c0, c1))
+    pid, psc = pid.cpu().numpy(), psc.cpu().numpy()
+    for u in range(U):
+        cand = nais_oracle.complement_candidates(data.history(u), P)
+        cand = cand[(cand >= c0) & (cand < c1)]
+        ref, _ = nais_oracle.forward_basic(p, np.broadcast_to(data.history(u), (len(cand), h[u])), cand)
+        rid, rsc = nais_oracle.topk_ids(cand, ref, K)
+        assert_topk_equivalent(rid, rsc, pid[u], psc[u], tie_ulps=TIE_ULPS,
+                               lookup=dict(zip(cand.tolist(), ref.tolist())))
+        did, dsc = nais_oracle.topk_ids(cand, full[u][cand], K)   # the direct route's block top-k
+        assert_topk_equivalent(did, dsc, pid[u], psc[u], tie_ulps=TIE_ULPS)
+    _stats("config 5", before)
