@@ -1984,6 +1984,8 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
   return check_launch("catalog_score_kernel");
 }
 
+constexpr size_t kLdsBytes = 160 * 1024;   // LDS per workgroup on gfx950 (MI355X_MICROARCH.md)
+
 template <int DH, int HB, int VAR, int NPC>
 size_t catalog_x3_lds() {
   constexpr bool DIST = VarT<VAR>::DIST;
@@ -2001,6 +2003,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
                                        scores, ld, nan_count, stream, tab);
   } else {
     const size_t lds = catalog_x3_lds<DH, HB, VAR, NPC>();
+    if (lds > kLdsBytes) return fail(NAIS_E_INVALID, "catalog_score_x3_kernel: shape exceeds LDS");
     auto kern = catalog_score_x3_kernel<DH, HB, VAR, NPC>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -2023,8 +2026,10 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
-  } else if constexpr (VarT<VAR>::DIST || (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32))) {
-    // the distance features ride on the per-pair split kernel (also in pair-table mode)
+  } else if constexpr (VarT<VAR>::DIST || (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32)) ||
+                       CfgB<DH, HB, false, WAVES, NPC>::BYTES > kLdsBytes) {
+    // the distance features ride on the per-pair split kernel (also in pair-table mode); so do
+    // shapes whose item ring does not fit the LDS (fp16x6 at D = H = 128: 2 x 96 KiB per item)
     return launch_catalog_x3<DH, HB, VAR, NPC>(d, indptr, indices, users, nb, region_of, coords,
                                                latlon_mat, scores, ld, nan_count, stream, tab);
   } else {

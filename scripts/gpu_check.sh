@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=10 -q -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 tail -5 gpurun_out/pytest_gpu.log

