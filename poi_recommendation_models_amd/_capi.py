@@ -28,7 +28,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
            "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
            "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
-           "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish")
+           "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
+           "nais_pair_table_il", "nais_pair_gather_topk_l2")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -194,6 +195,12 @@ def load(path: str | None = None):
     lib.nais_pair_gather_topk.restype = i32
     lib.nais_pair_gather_topk.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp,
                                           vp]
+    lib.nais_pair_table_il.restype = i32
+    lib.nais_pair_table_il.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp,
+                                       i64, vp]
+    lib.nais_pair_gather_topk_l2.restype = i32
+    lib.nais_pair_gather_topk_l2.argtypes = [vp, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp,
+                                             vp, vp, i32, i32, vp]
     lib.nais_topk_keys_finish.restype = i32
     lib.nais_topk_keys_finish.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32

@@ -11,6 +11,7 @@ per user. Nothing per-candidate crosses PCIe.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -239,6 +240,13 @@ PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 # 542.6 / 552.6 / 614.8 ms while the gather stream's own time fell only 539 -> 532 ms
 # (profiles/r1/table_gather_frac/; results bit-identical, test_pairs_blocks_passes_bit_identical).
 PAIR_TABLE_GATHER_FRAC = 0.0
+# L2-blocked fused gather (nais_pair_gather_topk_l2 over one interleaved chunk-major table): each
+# wave keeps up to 32 users' sums of a 64-column chunk in registers while all waves walk the table
+# in blocks of PAIR_L2_ROWS rows (~1.5 MB), so the rows shared by ~50 users come from the XCD's L2
+# rather than the Infinity Cache. Same sums in the same order as nais_pair_gather_topk.
+PAIR_L2_GATHER = os.environ.get("NAIS_PAIR_L2", "0") == "1"   # A/B: slower so far
+PAIR_L2_ROWS = int(os.environ.get("NAIS_PAIR_L2_ROWS", "3072"))
+PAIR_L2_WAVES_PER_CU = int(os.environ.get("NAIS_PAIR_L2_WAVES_PER_CU", "20"))
 _masked: dict = {}
 
 
@@ -369,6 +377,17 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     from .model import _NAISDevice
     fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256
              and type(model)._pair_fixup is _NAISDevice._pair_fixup)
+    # the L2-blocked gather reads the interleaved table that nais_pair_table_il writes (the NAIS
+    # catalog kernels; other cores keep the two row-major tables)
+    l2 = fused and PAIR_L2_GATHER and type(model)._pair_table is _NAISDevice._pair_table
+
+    def table(tab, c0, w, stream_):
+        if l2:
+            model._pair_table_il(lib, prm, items, J, c0, w, reg, cor, llm, tab.data_ptr(), J * 128,
+                                 stream_)
+        else:
+            model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
+                              tab[1].data_ptr(), W, stream_)
     # users per pass: their score rows take at most half the budget (fused: no score rows)
     per_pass = n if (rows_only or fused) else max(1, min(n, (budget // 2) // (4 * NC)))
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
@@ -379,8 +398,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
-        def gather_launches(w):   # nais_pair_gather_topk launches one kernel per 256-column stripe
-            return (w + PAIR_STRIPE - 1) // PAIR_STRIPE if fused else 1
+        def gather_launches(w):   # one fused-gather kernel per 256-column stripe / 64-column chunk
+            return (w + (64 if l2 else PAIR_STRIPE) - 1) // (64 if l2 else PAIR_STRIPE) if fused else 1
         if fused:
             keys = torch.empty(m, k, dtype=torch.int64, device=dev)
             kcount = torch.zeros(m, dtype=torch.int32, device=dev)
@@ -388,6 +407,13 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             def gather(tab, c0, w, stream_, a=0, b=None):   # launch slots [a, b) of u_dev
                 b = m if b is None else b
                 if b <= a:
+                    return
+                if l2:
+                    _capi.check(lib.nais_pair_gather_topk_l2(
+                        tab.data_ptr(), J * 128, J, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                        csr.indices.data_ptr(), u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta),
+                        k, keys.data_ptr() + 8 * k * a, kcount.data_ptr() + 4 * a, counters[0:1].data_ptr(),
+                        PAIR_L2_ROWS, gather_waves, stream_), "nais_pair_gather_topk_l2")
                     return
                 _capi.check(lib.nais_pair_gather_topk(
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
@@ -412,16 +438,16 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             if events is not None:
                 events.append(("table_cus", None, None, table_cus))
             overlap = 0 < table_cus < ncu and len(blocks) > 1 and stream is None
-            tabs = [torch.empty(2, J, W, dtype=torch.float32, device=dev)
+            gather_waves = (ncu - table_cus if overlap else ncu) * PAIR_L2_WAVES_PER_CU
+            shape = ((W + 63) // 64, J, 128) if l2 else (2, J, W)
+            tabs = [torch.empty(*shape, dtype=torch.float32, device=dev)
                     for _ in range(2 if overlap else 1)]
             if overlap:
                 ts, gs = _masked_streams(dev, table_cus)
                 first_all = PAIR_FIRST_TABLE_ALL_CUS
                 if first_all:      # block 0's table alone, on the caller's stream (all CUs)
                     w0 = min(W, c1_all - blocks[0])
-                    timed("table", lambda: model._pair_table(lib, prm, items, J, blocks[0], w0, reg, cor, llm,
-                                                             tabs[0][0].data_ptr(), tabs[0][1].data_ptr(),
-                                                             W, st))
+                    timed("table", lambda: table(tabs[0], blocks[0], w0, st))
                 ts.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
                 done_g = [None, None]
@@ -444,8 +470,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     if not (b == 0 and first_all):
                         e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e_t0.record(ts)
-                        model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
-                                          tab[1].data_ptr(), W, ts.cuda_stream)
+                        table(tab, c0, w, ts.cuda_stream)
                         e_t1.record(ts)
                         gs.wait_event(e_t1)
                         if events is not None:
@@ -460,8 +485,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     if m1 < m:   # the tail users, behind this block's table on the table stream
                         gather(tab, c0, w, ts.cuda_stream, m1, m)
                     continue
-                timed("table", lambda: model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm,
-                                                         tab[0].data_ptr(), tab[1].data_ptr(), W, st))
+                timed("table", lambda: table(tab, c0, w, st))
                 timed("gather", lambda: gather(tab, c0, w, st), gather_launches(w))
             if overlap:
                 torch_stream.wait_stream(gs)

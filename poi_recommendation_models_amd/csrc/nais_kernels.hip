@@ -96,7 +96,20 @@ struct TableOut {
   float* es = nullptr;
   int64_t ld = 0, col0 = 0, cols = 0, nitems = 0;
   int32_t gi = 0;
+  // cs > 0: one interleaved, chunk-major table instead of two row-major ones (the L2-blocked
+  // gather's layout): (e, es) of (row r, column offset x) at e[(x / 64) * cs + r * 128 + (x % 64) * 2]
+  int64_t cs = 0;
 };
+// the pair's two terms for item row `row` (relative to the launch's base) and column offset x
+__device__ __forceinline__ void tab_put(const TableOut& t, int64_t row, int64_t x, float e, float es) {
+  if (t.cs) {
+    *reinterpret_cast<float2*>(t.e + (x >> 6) * t.cs + row * 128 + (x & 63) * 2) = make_float2(e, es);
+  } else {
+    const int64_t o = row * t.ld + x;
+    tab_store(t.e + o, e);
+    tab_store(t.es + o, es);
+  }
+}
 
 #ifndef NAIS_TILE_MAJOR
 #define NAIS_TILE_MAJOR 0
@@ -397,9 +410,7 @@ catalog_score_kernel(DevParams p, const int64_t* __restrict__ indptr,
       const float e = expf(a) * (keep ? 1.f : 0.f);        // model.py:75-78 (inf * 0 -> NaN)
       if (tab.e) {
         if (valid && hh == 0) {
-          const int64_t o = (hbeg + j0 + jj) * tab.ld + (c - tab.col0);
-          tab_store(tab.e + o, e);
-          tab_store(tab.es + o, e * s);
+          tab_put(tab, hbeg + j0 + jj, c - tab.col0, e, e * s);
         }
         continue;
       }
@@ -935,9 +946,7 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
       const float e = expf(a) * (keep ? 1.f : 0.f);
       if (tab.e) {   // pair-table mode: the pair's two terms instead of the user's sums
         if (valid && hh == 0) {
-          const int64_t o = (hbeg + j0 + jj) * tab.ld + (c - tab.col0);
-          tab_store(tab.e + o, e);
-          tab_store(tab.es + o, e * sv);
+          tab_put(tab, hbeg + j0 + jj, c - tab.col0, e, e * sv);
         }
         continue;
       }
@@ -969,6 +978,9 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // candidate into B fragments that stay in VGPRs for the whole sweep. The per-(c, j) VALU work
 // is then only the epilogue and h_j . t_c -- no per-pair conversions.
 // ---------------------------------------------------------------------------------------------
+#ifndef NAIS_X3B_PIPE6
+#define NAIS_X3B_PIPE6 1
+#endif
 template <int DH, int HB, bool DIST, int NW = WAVES, int NPC = 2>
 struct CfgB {
   static constexpr int D = 2 * DH;
@@ -991,10 +1003,15 @@ struct CfgB {
 #ifdef NAIS_X3B_NOPIPE
   static constexpr bool PIPE = false;   // debug: the wide epilogue structure for every shape
 #else
-  static constexpr bool PIPE = NPC == 2 && HB <= 2 && DH <= 32;
+  // fp16x6 (NPC = 3) pipelines too, with b1 / w2 read from LDS (EREGS = false) to stay within
+  // 256 VGPRs; without the pipeline the per-group barrier lines up both waves of a SIMD, so their
+  // MFMA and VALU phases coincide instead of overlapping
+  static constexpr bool PIPE = (NPC == 2 || NAIS_X3B_PIPE6) && HB <= 2 && DH <= 32;
 #endif
+  static constexpr bool EREGS = PIPE && NPC == 2;   // b1 / w2 pre-scaled in VGPRs
   static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
                                   size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+  static_assert(!PIPE || G % 2 == 0, "the pipelined steps alternate two accumulator sets per item");
 };
 
 // NW = waves per workgroup (2 per SIMD at 8). D, H <= 64 pipeline the epilogue (CfgB::PIPE).
@@ -1115,7 +1132,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float S = 0.f, N = 0.f;
   bool in_hist = false;
   // b1 / w2 pre-scaled in VGPRs when pipelined; read from LDS (unscaled, one fma per use) when wide
-  Epi16<HB, PIPE> epi;
+  Epi16<HB, C::EREGS> epi;
 
   // build the fragments of chunk-local item jj into ring slot (grp, it)
   // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
@@ -1175,9 +1192,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     if (live) {
       if (tab.e) {
         if (valid && hh == 0) {
-          const int64_t o = (hbeg + j0 + pj) * tab.ld + (c - tab.col0);
-          tab_store(tab.e + o, e);
-          tab_store(tab.es + o, e * sv);
+          tab_put(tab, hbeg + j0 + pj, c - tab.col0, e, e * sv);
         }
       } else {
         in_hist |= !keep;
@@ -1296,7 +1311,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   };
 
   float SAcur = 1.f;
-  floatx16 accP[HB];
+  floatx16 acc2[2][HB];   // PIPE: the accumulators of even / odd chunk-local items
   for (j0 = 0; j0 < hlen; j0 += JCB) {
     const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
     __syncthreads();
@@ -1371,12 +1386,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       for (int it = 0; it < G; ++it) {
         const int jj = g * G + it;
         if (jj < jn) {
-          floatx16 accN[HB];
           const uint4* src = ring + (((g & 1) * G + it) * NPC) * NE;
-          if constexpr (PIPE) {
-            step(std::true_type{}, std::true_type{}, src, accN, accP, jj, prev, prev >= 0);
-#pragma unroll
-            for (int hb = 0; hb < HB; ++hb) accP[hb] = accN[hb];
+          if constexpr (PIPE) {   // item jj into acc2[jj & 1] (G even: static), item jj - 1 from the other
+            step(std::true_type{}, std::true_type{}, src, acc2[it & 1], acc2[(it + 1) & 1], jj, prev,
+                 prev >= 0);
             prev = jj;
           } else {
             if (NAIS_X3B_WIDE_ILV && g + 1 < ngroups && (g + 1) * G + it < jn)
@@ -1388,8 +1401,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       __syncthreads();
     }
     if (PIPE && prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
-      floatx16 accN[HB];
-      step(std::false_type{}, std::true_type{}, ring, accN, accP, 0, prev, true);
+      if (prev & 1)
+        step(std::false_type{}, std::true_type{}, ring, acc2[0], acc2[1], 0, prev, true);
+      else
+        step(std::false_type{}, std::true_type{}, ring, acc2[1], acc2[0], 0, prev, true);
     }
   }
   if (tab.e) return;
@@ -2246,18 +2261,22 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
   return NAIS_OK;
 }
 
-int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
-                        int64_t col0, int64_t cols, const int64_t* region_of,
-                        const double* coords, const double* latlon_mat, float* e, float* es,
-                        int64_t ld, void* stream) {
+namespace {
+// nais_pair_table / nais_pair_table_il: cs = 0 -> two row-major tables (e, es, ld), cs > 0 -> one
+// interleaved chunk-major table (e; es unused)
+int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                        int64_t col0, int64_t cols, const int64_t* region_of, const double* coords,
+                        const double* latlon_mat, float* e, float* es, int64_t ld, int64_t cs,
+                        void* stream) {
   Shape sh;
   int rc = validate(params, &sh);
   if (rc) return rc;
   if (num_items < 0 || col0 < 0 || cols < 0 || col0 + cols > params->num_pois)
     return fail(NAIS_E_INVALID, "bad item count or column range");
   if (num_items == 0 || cols == 0) return NAIS_OK;
-  if (!items || !e || !es) return fail(NAIS_E_INVALID, "missing pointer");
-  if (ld < cols) return fail(NAIS_E_INVALID, "ld < cols");
+  if (!items || !e || (!cs && !es)) return fail(NAIS_E_INVALID, "missing pointer");
+  if (!cs && ld < cols) return fail(NAIS_E_INVALID, "ld < cols");
+  if (cs && cs < num_items * 128) return fail(NAIS_E_INVALID, "chunk_stride < num_items * 128");
   if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
       !region_of)
     return fail(NAIS_E_INVALID, "region variants need region_of");
@@ -2271,13 +2290,14 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
   TableOut tab;
   tab.ld = ld;
   tab.cols = cols;
+  tab.cs = cs;
   tab.gi = PAIR_GROUP_ITEMS;
   const int64_t groups_per_launch = 65535;
   for (int64_t g0 = 0; g0 * tab.gi < num_items; g0 += groups_per_launch) {
     const int64_t base = g0 * tab.gi;
     tab.nitems = std::min<int64_t>(num_items - base, groups_per_launch * tab.gi);
-    tab.e = e + base * ld;
-    tab.es = es + base * ld;
+    tab.e = e + base * (cs ? 128 : ld);
+    tab.es = cs ? nullptr : es + base * ld;
     tab.col0 = col0;
     const int ng = (int)((tab.nitems + tab.gi - 1) / tab.gi);
     if (params->precision == NAIS_PRECISION_FP32)
@@ -2293,6 +2313,24 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
     if (rc) return rc;
   }
   return NAIS_OK;
+}
+}  // namespace
+
+int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                        int64_t col0, int64_t cols, const int64_t* region_of,
+                        const double* coords, const double* latlon_mat, float* e, float* es,
+                        int64_t ld, void* stream) {
+  return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, e, es,
+                         ld, 0, stream);
+}
+
+int32_t nais_pair_table_il(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                           int64_t col0, int64_t cols, const int64_t* region_of,
+                           const double* coords, const double* latlon_mat, float* table,
+                           int64_t chunk_stride, void* stream) {
+  if (chunk_stride <= 0) return fail(NAIS_E_INVALID, "chunk_stride must be > 0");
+  return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, table,
+                         nullptr, 0, chunk_stride, stream);
 }
 
 int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,

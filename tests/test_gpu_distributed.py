@@ -71,3 +71,48 @@ def test_distributed_topk_two_ranks_equal_single(kind, plan):
             assert str(r["plan"]) == plan
             np.testing.assert_array_equal(r["ids"], ids.cpu().numpy())
             np.testing.assert_array_equal(r["sc"], sc.cpu().numpy())
+
+
+def _positives(data, seed):
+    rng = np.random.default_rng(seed)
+    return [[int(x) for x in rng.choice(data.num_pois, 5, replace=False)] for _ in range(data.num_users)]
+
+
+def _worker_validation(rank, world, port, kind, out):
+    """validation.NAIS_validation itself, called by every rank inside the process group."""
+    import torch.distributed as dist
+    from poi_recommendation_models_amd import validation as V
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    data, p = _data(kind)
+    m = _model(p, data.num_pois)
+
+    class Args:
+        topk = 50
+    got = V.NAIS_validation(m, Args(), data.num_users, _positives(data, 1), _positives(data, 2),
+                            data.to_scipy(), [5, 10, 20, 50])
+    np.savez(f"{out}_{rank}.npz", got=np.array(got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["shared", "sparse"])
+def test_validation_autoroute_two_ranks_equal_single(kind):
+    """run.py:112-116 unchanged under torchrun: NAIS_validation in a 2-rank group (column-sharded
+    pairs or user-sharded route) returns the single-process 6-tuple on every rank."""
+    import torch.multiprocessing as mp
+    from poi_recommendation_models_amd import validation as V
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "v")
+        mp.start_processes(_worker_validation, args=(2, _free_port(), kind, out), nprocs=2, join=True,
+                           start_method="spawn")
+        res = [np.load(f"{out}_{r}.npz")["got"] for r in range(2)]
+    data, p = _data(kind)
+    m = _model(p, data.num_pois)
+
+    class Args:
+        topk = 50
+    ref = np.array(V.NAIS_validation(m, Args(), data.num_users, _positives(data, 1),
+                                     _positives(data, 2), data.to_scipy(), [5, 10, 20, 50]))
+    for r in res:
+        np.testing.assert_array_equal(r, ref)

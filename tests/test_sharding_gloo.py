@@ -8,7 +8,7 @@ import socket
 import numpy as np
 import torch
 
-from _helpers import load_golden, params_from
+from _helpers import load_golden, params_from, positives_from
 from oracle import nais_oracle
 from poi_recommendation_models_amd.sharding import gather_topk, shard_users
 
@@ -116,3 +116,69 @@ def test_sharded_table_allgather_world2():
         assert pr.exitcode == 0
     assert all(r[1] and r[2] for r in res)
     np.testing.assert_array_equal(res[0][3], res[1][3])   # MLP broadcast from rank 0
+
+
+def _worker_validation(rank, world, port, q):
+    """validation.NAIS_validation inside a world-2 gloo group routes to sharding.distributed_topk
+    (run.py:112-116 unchanged). The device scorer is replaced by the oracle here (CPU test); the
+    user sharding, the all-gather of the [users, k] blocks and the metrics are the product code."""
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from poi_recommendation_models_amd import sharding
+    from poi_recommendation_models_amd import validation as V
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = load_golden("catalog_basic.npz")
+    p = params_from(z, "trained")
+    P, U = int(z["num_pois"]), int(z["num_users"])
+    calls = []
+
+    def oracle_distributed_topk(model, train_matrix, num_users, k, group=None, **kw):
+        calls.append(num_users)
+        hl = np.diff(train_matrix.indptr)[:num_users]
+        mine = shard_users(hl, P, dist.get_world_size(group))[dist.get_rank(group)]
+        ids, sc = [], []
+        for u in mine:
+            hist = train_matrix.indices[train_matrix.indptr[u]:train_matrix.indptr[u + 1]]
+            i, t = nais_oracle.topk_ids(*nais_oracle.catalog_scores_basic(p, hist, P), k)
+            ids.append(i)
+            sc.append(t)
+        return gather_topk(mine, torch.as_tensor(np.array(ids).reshape(-1, k)),
+                           torch.as_tensor(np.array(sc, dtype=np.float32).reshape(-1, k)),
+                           num_users, group=group)
+    sharding.distributed_topk = oracle_distributed_topk
+
+    class Model:                      # what _recommend_ids touches on the module
+        report_nan = False
+        _last_nan = torch.zeros((), dtype=torch.int32)
+
+        def eval(self):
+            return self
+
+    class Args:
+        topk = 50
+    X = sp.csr_matrix((np.ones(len(z["indices"])), z["indices"], z["indptr"]), shape=(U, P))
+    got = V.NAIS_validation(Model(), Args(), U, positives_from(z, "test"), positives_from(z, "val"),
+                            X, [5, 10, 15, 20, 25, 30])
+    q.put((rank, calls, np.array(got)))
+    dist.destroy_process_group()
+
+
+def test_validation_autoroutes_world2():
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_validation, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    z = load_golden("catalog_basic.npz")
+    U = int(z["num_users"])
+    for rank, calls, got in res:
+        assert calls == [U], calls                          # went through the distributed path
+        np.testing.assert_allclose(got, z["trained/metrics"], atol=2.0 / U)
+    np.testing.assert_array_equal(res[0][2], res[1][2])     # the same 6-tuple on every rank
