@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=50)
     ap.add_argument("--precision", default="fp16x6", choices=sorted(PRODUCTS))
     ap.add_argument("--no-fp32-leg", action="store_true",
-                    help="skip the secondary exact-fp32 and fp16x3 timings ('fp32_path', 'fp16x3_path')")
+                    help="skip the secondary legs (fp32_path, fp16x3_path, prior_path, region_distance_path)")
     ap.add_argument("--leg-steps", type=int, default=3, help="timed steps of each secondary leg")
     ap.add_argument("--cpu-users", type=int, default=32,
                     help="CPU baseline sample: the first N users (after a 1-user warm-up)")
@@ -408,6 +408,22 @@ def main():
         dist.destroy_process_group()
 
 
+PRIOR_A, PRIOR_B, PRIOR_ALPHA = 0.052, -1.37, 0.2   # a typical PowerLaw fit (a, b) and run.py's alpha
+
+
+def variant_leg(name, job, steps, pairs_job, dev):
+    """One warm-up and `steps` timed whole jobs of a secondary configuration (same users / POIs)."""
+    job()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        job()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    return {"value": pairs_job * steps / el, "unit": "pairs/s", "steps": steps, "warmup": 1,
+            "ms_per_step": el / steps * 1e3}
+
+
 def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
     from poi_recommendation_models_amd import catalog
@@ -592,6 +608,28 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                           "table_peak_tflops": t_l["peak"], "table_cus": t_l["cus"],
                           "gather_ms_per_step": g_l["ms_per_step"]}
         model.precision = a.precision
+        legs["prior"] = variant_leg("prior", lambda: _score_topk_pairs(
+            model, csr, users, K, None, None, None, None, force=True,
+            prior=(PRIOR_A, PRIOR_B, PRIOR_ALPHA, data.place_coords)), a.leg_steps, pairs_job, dev)
+        legs["prior"]["what"] = ("the same job ranked on the power-law-blended score (run.py:537-539): "
+                                 "pr_d(dist) pair table + float64 product gather per user, score rows, "
+                                 "nais_topk_blend_rows; a, b, alpha = %g, %g, %g" % (PRIOR_A, PRIOR_B, PRIOR_ALPHA))
+        from poi_recommendation_models_amd.model import NAIS_region_distance_Embedding
+        from poi_recommendation_models_amd.synthetic import init_nais_params as _init
+        rd = NAIS_region_distance_Embedding(P, D, H, 0.5, 1024, 1)
+        rd.load_state_dict({k: torch.from_numpy(v) for k, v in
+                            _init(P, D, H, seed=11, emb_std=0.3, bias_std=0.1, variant="region_distance",
+                                  num_regions=1024).items()}, strict=False)
+        rd = rd.to(dev).eval()
+        rd.report_nan = False
+        rd.precision = a.precision
+        legs["region_distance"] = variant_leg("region_distance", lambda: _score_topk_pairs(
+            rd, csr, users, K, data.region_of, data.place_coords, None, None, force=True),
+            a.leg_steps, pairs_job, dev)
+        legs["region_distance"]["what"] = ("NAIS_region_distance_Embedding (model.py:246-297) on the same "
+                                           "users / POIs: [h | region] rows, distance features from the POI "
+                                           "coordinates, %s tables" % a.precision)
+        del rd
     check = None
     if world == 1 and emulate == 1 and not a.no_self_check and rank == 0:
         ids, sc = last["out"]
@@ -636,6 +674,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "self_check": check,
             "fp32_path": legs.get("fp32"),
             "fp16x3_path": legs.get("fp16x3"),
+            "prior_path": legs.get("prior"),
+            "region_distance_path": legs.get("region_distance"),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

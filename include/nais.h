@@ -260,6 +260,32 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
                               uint64_t* keys, int32_t* kcount, int32_t* nan_count, void* stream);
 int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,
                               int32_t* out_ids, float* out_scores, int32_t* short_count, void* stream);
+/*
+ * Power-law prior on the pairs route (powerLaw.py:86-92, run.py:537-539; the direct route's
+ * nais_score_topk with a prior computes the same G rows per user):
+ *   nais_pair_prior_table   pr[r*ld + c-col0] = pr_d(dist(items[r], c)) (float64, powerLaw.py's
+ *                           operation order) for r < num_items, c in [col0, col0 + cols).
+ *   nais_pair_prior_gather  per user slot and c in [col0, col0 + cols):
+ *                           g[slot*g_ld + c-g_col0] = prod_j pr[row(j), c] over the history in CSR
+ *                           order (1.0 for an empty history; -1.0 for history POIs) -- the bits of
+ *                           nais_powerlaw_prior -- and gmax_bits[slot] = max(gmax_bits[slot], the
+ *                           block's largest candidate value) as u64 bits; zero gmax_bits before the
+ *                           first block.
+ *   nais_topk_blend_rows    top-k of f32((1 - alpha) * score) + alpha * g / gmax (float64; history
+ *                           POIs, score < 0, excluded) per row, (score desc, id asc), as
+ *                           nais_score_topk ranks with a prior; out_scores = the blended score as f32.
+ */
+int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int64_t* items,
+                              int64_t num_items, int64_t col0, int64_t cols, double a, double b,
+                              double* pr, int64_t ld, void* stream);
+int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowmap,
+                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                               int32_t num_users, int64_t col0, int64_t cols, double* g, int64_t g_ld,
+                               int64_t g_col0, uint64_t* gmax_bits, void* stream);
+int32_t nais_topk_blend_rows(const float* scores, int64_t score_ld, const double* g, int64_t g_ld,
+                             const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
+                             double alpha, int32_t* out_ids, float* out_scores, int32_t* short_count,
+                             void* stream);
 int32_t nais_pair_table_il(const nais_params_t* params, const int64_t* items, int64_t num_items,
                            int64_t col0, int64_t cols, const int64_t* region_of,
                            const double* coords, const double* latlon_mat, float* table,

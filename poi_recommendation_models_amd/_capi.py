@@ -29,7 +29,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
            "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
            "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
-           "nais_pair_table_il", "nais_pair_gather_topk_l2")
+           "nais_pair_table_il", "nais_pair_gather_topk_l2", "nais_pair_prior_table",
+           "nais_pair_prior_gather", "nais_topk_blend_rows")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -201,6 +202,12 @@ def load(path: str | None = None):
     lib.nais_pair_gather_topk_l2.restype = i32
     lib.nais_pair_gather_topk_l2.argtypes = [vp, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp,
                                              vp, vp, i32, i32, vp]
+    lib.nais_pair_prior_table.restype = i32
+    lib.nais_pair_prior_table.argtypes = [vp, i64, vp, i64, i64, i64, f64, f64, vp, i64, vp]
+    lib.nais_pair_prior_gather.restype = i32
+    lib.nais_pair_prior_gather.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, vp, i64, i64, vp, vp]
+    lib.nais_topk_blend_rows.restype = i32
+    lib.nais_topk_blend_rows.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp]
     lib.nais_topk_keys_finish.restype = i32
     lib.nais_topk_keys_finish.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32

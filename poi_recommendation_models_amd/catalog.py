@@ -134,8 +134,9 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
 
     `strategy` (default: the model's `catalog_strategy`, "auto"): "direct" runs the fused per-user
     kernels; "pairs" computes each (distinct history POI, candidate) term once and gathers every
-    user's sums from those tables (nais_pair_*); "auto" picks "pairs" when the users' history
-    entries outnumber their distinct POIs by PAIR_MIN_SHARING and there is no prior.
+    user's sums from those tables (nais_pair_*; with a prior also the pr_d(dist) table and each
+    user's float64 product G, nais_pair_prior_*); "auto" picks "pairs" when the users' history
+    entries outnumber their distinct POIs by PAIR_MIN_SHARING.
 
     `stream` (a raw hipStream_t handle): the whole call -- its allocations, uploads, kernels and
     the final reorder -- runs on that stream, which first waits for the caller's current stream;
@@ -159,9 +160,9 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
         if prior is not None:
             raise NotImplementedError(f"{type(model).__name__}: no power-law prior on its catalog path")
         strategy = "pairs"
-    if strategy != "direct" and prior is None:
+    if strategy != "direct":
         got = _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat,
-                                stream, force=strategy == "pairs")
+                                stream, force=strategy == "pairs", prior=prior)
         if got is not None:
             return got
     csr = device_csr(train_matrix, dev)
@@ -316,10 +317,12 @@ def _masked_streams(dev, table_cus):
 
 
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
-                      rows_only=False, cols=None, events=None):
+                      rows_only=False, cols=None, events=None, prior=None):
     """Pairs strategy. `cols` = (c0, c1): score only POIs [c0, c1) (top-k ids are global POI ids;
     a column shard of sharding.distributed_topk_pairs). `events`: optional list that receives
-    (kind, start, end) HIP events around every table / gather / top-k launch."""
+    (kind, start, end) HIP events around every table / gather / top-k launch. `prior` = (a, b,
+    alpha, poi_coords): rank on the power-law-blended score (score_topk); score rows + float64 G
+    rows per pass, then nais_topk_blend_rows (the direct route's blend, same G bits)."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model._item_tables()[0].shape[0]
@@ -375,8 +378,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     free = torch.cuda.mem_get_info(dev)[0]
     budget = int(free * PAIR_MEMORY_FRACTION)
     from .model import _NAISDevice
-    fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256
+    if prior is not None and (cols is not None or rows_only or model._pairs_only):
+        raise NotImplementedError("the pairs route blends the prior over whole rows of NAIS models only")
+    fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256 and prior is None
              and type(model)._pair_fixup is _NAISDevice._pair_fixup)
+    if prior is not None:
+        pa, pb, alpha, pc = prior
+        pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
+    pr_of = {}   # column-block table -> its float64 pr_d table (prior only)
     # the L2-blocked gather reads the interleaved table that nais_pair_table_il writes (the NAIS
     # catalog kernels; other cores keep the two row-major tables)
     l2 = fused and PAIR_L2_GATHER and type(model)._pair_table is _NAISDevice._pair_table
@@ -388,8 +397,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         else:
             model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
                               tab[1].data_ptr(), W, stream_)
-    # users per pass: their score rows take at most half the budget (fused: no score rows)
-    per_pass = n if (rows_only or fused) else max(1, min(n, (budget // 2) // (4 * NC)))
+        if prior is not None:
+            _capi.check(lib.nais_pair_prior_table(pri_coords.data_ptr(), P, items.data_ptr(), J, c0, w,
+                                                  float(pa), float(pb), pr_of[id(tab)].data_ptr(), W,
+                                                  stream_), "nais_pair_prior_table")
+    # users per pass: their score rows (+ float64 G rows with a prior) take at most half the
+    # budget (fused: no score rows)
+    row_bytes = 4 * NC + (8 * NC if prior is not None else 0)
+    per_pass = n if (rows_only or fused) else max(1, min(n, (budget // 2) // row_bytes))
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
     sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -422,12 +437,20 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     stream_), "nais_pair_gather_topk")
         else:
             scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
+            if prior is not None:
+                G = torch.empty(m, NC, dtype=torch.float64, device=dev)
+                gmax = torch.zeros(m, dtype=torch.int64, device=dev)
 
             def gather(tab, c0, w, stream_, a=0, b=None):
                 _capi.check(lib.nais_pair_gather(
                     tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
                     scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), stream_), "nais_pair_gather")
+                if prior is not None:
+                    _capi.check(lib.nais_pair_prior_gather(
+                        pr_of[id(tab)].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                        csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, G.data_ptr(), NC, c0_all,
+                        gmax.data_ptr(), stream_), "nais_pair_prior_gather")
         if J > 0:
             W = min(PAIR_BLOCK_COLS, (budget // 4) // (8 * J))
             W = int(min(NC, max(256, W // 256 * 256)))
@@ -442,6 +465,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             shape = ((W + 63) // 64, J, 128) if l2 else (2, J, W)
             tabs = [torch.empty(*shape, dtype=torch.float32, device=dev)
                     for _ in range(2 if overlap else 1)]
+            if prior is not None:
+                pr_of.update({id(t): torch.empty(J, W, dtype=torch.float64, device=dev) for t in tabs})
             if overlap:
                 ts, gs = _masked_streams(dev, table_cus)
                 first_all = PAIR_FIRST_TABLE_ALL_CUS
@@ -490,10 +515,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             if overlap:
                 torch_stream.wait_stream(gs)
                 torch_stream.wait_stream(ts)
-                for t in tabs:      # the allocator must not hand these to the main stream early
+                for t in [*tabs, *pr_of.values()]:   # not handed to the main stream early
                     t.record_stream(ts)
                     t.record_stream(gs)
             del tabs
+            pr_of.clear()
             if not fused:
                 model._pair_fixup(csr, u_dev, m, scores, c0_all, c1_all, st)
         else:
@@ -507,9 +533,19 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(), st), "nais_topk_keys_finish"))
             del keys, kcount
             continue
-        timed("topk", lambda: _capi.check(lib.nais_topk_rows(
-            scores.data_ptr(), NC, NC, m, k, ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(),
-            counters[1:2].data_ptr(), st), "nais_topk_rows"))
+        if prior is not None:
+            if J == 0:      # empty histories: G = prod over nothing = 1.0 for every candidate
+                G.fill_(1.0)
+                gmax.fill_(int(np.array(1.0).view(np.int64)))
+            timed("topk", lambda: _capi.check(lib.nais_topk_blend_rows(
+                scores.data_ptr(), NC, G.data_ptr(), NC, gmax.data_ptr(), NC, m, k, float(alpha),
+                ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(),
+                st), "nais_topk_blend_rows"))
+            del G, gmax
+        else:
+            timed("topk", lambda: _capi.check(lib.nais_topk_rows(
+                scores.data_ptr(), NC, NC, m, k, ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(),
+                counters[1:2].data_ptr(), st), "nais_topk_rows"))
         del scores
     model._last_nan = counters[0:1]
     ids = ids_out.to(torch.int64)

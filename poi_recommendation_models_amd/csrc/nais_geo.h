@@ -1,7 +1,7 @@
 // nais_geo.h -- powerLaw.dist (powerLaw.py:7-21) on the device, float64 in the reference's
 // operation order; every product/sum an explicit round-to-nearest op (__dmul_rn / __dadd_rn /
 // __dsub_rn) so the compiler cannot contract FMAs. Shared by the prior kernel (nais_kernels.hip)
-// and the pair-distance kernel (nais_disent.hip).
+// the pair-distance kernel (nais_disent.hip) and the prior pair tables (nais_pairs.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -27,9 +27,16 @@ __device__ __forceinline__ double ref_dist(const Geo& p1, const Geo& p2) {
   return __dmul_rn(acos(cosv), 6371.0);
 }
 
+// PowerLaw.pr_d (powerLaw.py:86-88): a * max(0.01, d) ** b   (Python max(0.01, nan) = 0.01)
+__device__ __forceinline__ double ref_pr_d(double a, double b, double d) {
+  const double dd = (d > 0.01) ? d : 0.01;
+  return __dmul_rn(a, pow(dd, b));
+}
+
 }  // namespace nais_geo
 
 using nais_geo::Geo;
 using nais_geo::make_geo;
 using nais_geo::ref_dist;
 using nais_geo::kD2R;
+using nais_geo::ref_pr_d;

@@ -728,6 +728,20 @@ struct Epi16<HB, false> {          // b1 / w2 read from LDS: acc starts at 0, un
   }
 };
 
+template <int HB>
+struct Epi16L {                    // per-wave LDS copy of S*b1 and w2/S (S wave-uniform): acc starts at S*b1
+  const float* pb;
+  const float* pw;
+  __device__ __forceinline__ void rescale(const float* mine, int hh, float, float) {
+    pb = mine + hh * HB * 16;
+    pw = mine + 2 * HB * 16 + hh * HB * 16;
+  }
+  __device__ __forceinline__ float init(int i) const { return pb[i]; }
+  __device__ __forceinline__ float term(int i, float acc, float) const {
+    return pw[i] * relu_bits(acc);
+  }
+};
+
 template <int DH, int HB, int VAR, int NPC>
 __global__ void __launch_bounds__(THREADS, 1)
 catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
@@ -981,6 +995,9 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #ifndef NAIS_X3B_PIPE6
 #define NAIS_X3B_PIPE6 1
 #endif
+#ifndef NAIS_X3B_WLDS
+#define NAIS_X3B_WLDS 1
+#endif
 template <int DH, int HB, bool DIST, int NW = WAVES, int NPC = 2>
 struct CfgB {
   static constexpr int D = 2 * DH;
@@ -990,7 +1007,11 @@ struct CfgB {
 #ifdef NAIS_X3B_G
   static constexpr int G = NAIS_X3B_G;
 #else
+#ifdef NAIS_X3B_G6   // A/B: items per ring group of the fp16x6 kernels
+  static constexpr int G = NPC == 3 ? NAIS_X3B_G6 : (IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1));
+#else
   static constexpr int G = IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1);   // items per ring group
+#endif
 #endif
   // LDS chunk rows; fp16x6 keeps 32 (the s tile below) even where 64 would fit
   static constexpr int JCB = (NPC == 3 || 2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;
@@ -1009,8 +1030,14 @@ struct CfgB {
   static constexpr bool PIPE = (NPC == 2 || NAIS_X3B_PIPE6) && HB <= 2 && DH <= 32;
 #endif
   static constexpr bool EREGS = PIPE && NPC == 2;   // b1 / w2 pre-scaled in VGPRs
-  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64 +
-                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+  // fp16x6 pipeline: one candidate scale S_t per WAVE (not per lane), so S = S_A * S_t is
+  // wave-uniform and each wave keeps S*b1 and w2/S in its own LDS slot (Epi16L): acc starts at
+  // S*b1 and the epilogue is relu + fma (3 VALU per value instead of 4), no VGPRs spent
+  static constexpr bool WLDS = NAIS_X3B_WLDS && PIPE && !EREGS;
+  static constexpr int ESCL = WLDS ? NW * EPI : 0;
+  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 +
+                                  size_t(ESCL) * 4 + 64 + size_t(JCB) * D * 4 + size_t(JCB) * 4 +
+                                  (DIST ? size_t(JCB) * 16 : 0);
   static_assert(!PIPE || G % 2 == 0, "the pipelined steps alternate two accumulator sets per item");
 };
 
@@ -1038,7 +1065,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][piece][NE]
   float* Adist = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);
   float* Eimg = Adist + C::ADIST;
-  float* red = Eimg + C::EPI;
+  float* Escl = Eimg + C::EPI;          // WLDS: per wave [S*b1 | w2/S] (EPI floats each)
+  float* red = Escl + C::ESCL;
   float* hrows = red + 16;
   int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
   double* hco = reinterpret_cast<double*>(hid + JCB);
@@ -1103,6 +1131,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
   for (int k = 0; k < DH; ++k) tmax = fmaxf(tmax, fabsf(tv[k]));
   tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+  if constexpr (C::WLDS) {   // one scale for the wave's 32 candidates (its pieces reach 2^-39 of it)
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+  }
   const float St = pow2_scale(tmax);
   const float invSt = 1.f / St;
   half8 tb[KS][NPC];
@@ -1132,7 +1164,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float S = 0.f, N = 0.f;
   bool in_hist = false;
   // b1 / w2 pre-scaled in VGPRs when pipelined; read from LDS (unscaled, one fma per use) when wide
-  Epi16<HB, C::EREGS> epi;
+  std::conditional_t<C::WLDS, Epi16L<HB>, Epi16<HB, C::EREGS>> epi;
 
   // build the fragments of chunk-local item jj into ring slot (grp, it)
   // build the fragments of chunk-local item jj into ring slot (grp, it); wv is pre-scaled by S_A
@@ -1367,7 +1399,13 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     SAcur = SA;
     Sacc = SA * St;
     invS = 1.f / Sacc;
-    epi.rescale(Eimg, hh, Sacc, invS);
+    if constexpr (C::WLDS) {   // this wave's S*b1 and w2/S (S is wave-uniform); the barrier
+      float* mine = Escl + wave * C::EPI;   // after the first builds publishes them
+      for (int f = lane; f < C::EPI; f += 64) mine[f] = Eimg[f] * (f < 2 * HB * 16 ? Sacc : invS);
+      epi.rescale(mine, hh, Sacc, invS);
+    } else {
+      epi.rescale(Eimg, hh, Sacc, invS);
+    }
     const int ngroups = (jn + G - 1) / G;
 #pragma unroll
     for (int it = 0; it < G; ++it)
@@ -1598,12 +1636,7 @@ topk_kernel(const float* __restrict__ scores, int64_t score_ld, int64_t P, int k
 // ---------------------------------------------------------------------------------------------
 // Geo, make_geo, ref_dist: nais_geo.h
 
-// PowerLaw.pr_d (powerLaw.py:86-88): a * max(0.01, d) ** b   (Python max(0.01, nan) = 0.01)
-__device__ __forceinline__ double ref_pr_d(double a, double b, double d) {
-  const double dd = (d > 0.01) ? d : 0.01;
-  return __dmul_rn(a, pow(dd, b));
-}
-
+// ref_pr_d (PowerLaw.pr_d): nais_geo.h
 constexpr int PRIOR_THREADS = 256;
 constexpr int PRIOR_JC = 256;
 
@@ -2414,6 +2447,29 @@ int32_t nais_powerlaw_prior(const double* coords, int64_t num_pois, const int64_
     const int rc = launch_prior(coords, num_pois, indptr, indices, users + u0, nb, a, b,
                                 out + (int64_t)u0 * out_ld, out_ld,
                                 reinterpret_cast<unsigned long long*>(out_max + u0), st);
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_topk_blend_rows(const float* scores, int64_t score_ld, const double* g, int64_t g_ld,
+                             const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
+                             double alpha, int32_t* out_ids, float* out_scores, int32_t* short_count,
+                             void* stream) {
+  if (num_rows < 0 || num_pois <= 0 || k <= 0 || score_ld < num_pois || g_ld < num_pois)
+    return fail(NAIS_E_INVALID, "bad shape");
+  if (k > MAX_K) return fail(NAIS_E_UNSUPPORTED, "k > 1024");
+  if (num_rows == 0) return NAIS_OK;
+  if (!scores || !g || !gmax_bits || !out_ids || !out_scores) return fail(NAIS_E_INVALID, "missing pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int32_t r0 = 0; r0 < num_rows; r0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_rows - r0);
+    hipLaunchKernelGGL(topk_blend_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores + (int64_t)r0 * score_ld,
+                       score_ld, g + (int64_t)r0 * g_ld, g_ld,
+                       reinterpret_cast<const unsigned long long*>(gmax_bits) + r0, num_pois, k,
+                       (float)(1.0 - alpha), alpha, out_ids + (int64_t)r0 * k, out_scores + (int64_t)r0 * k,
+                       short_count);
+    const int rc = check_launch("topk_blend_kernel");
     if (rc) return rc;
   }
   return NAIS_OK;

@@ -23,6 +23,7 @@
 
 #include "nais.h"
 #include "nais_internal.h"
+#include "nais_geo.h"
 
 namespace {
 
@@ -551,6 +552,93 @@ pair_gather_topk_l2_kernel(const float* __restrict__ T, int64_t nrows, int32_t r
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Power-law prior on the pairs route (powerLaw.py:86-92, run.py:537-539): pr_d(dist(j, c)) depends
+// on the pair only, so it is tabled once per (distinct history POI, candidate) like e and e*s,
+// and each user's G[c] = prod_j pr_d(dist(j, c)) is gathered as a float64 product in CSR order --
+// the operation order of prior_kernel (nais_powerlaw_prior), hence the same bits.
+constexpr int PRIOR_TAB_THREADS = 256;
+
+// pr[r * ld + c - col0] = pr_d(dist(items[r], c)) for r < nitems, c in [col0, col0 + cols)
+__global__ void __launch_bounds__(PRIOR_TAB_THREADS)
+prior_pair_table_kernel(const double* __restrict__ coords, const int64_t* __restrict__ items,
+                        int64_t nitems, int64_t col0, int64_t cols, double a, double b,
+                        double* __restrict__ pr, int64_t ld) {
+  constexpr int RB = 16;                     // item rows per workgroup (Geo of each in LDS)
+  __shared__ Geo hg[RB];
+  const int64_t x = int64_t(blockIdx.x) * PRIOR_TAB_THREADS + threadIdx.x;
+  const int64_t r0 = int64_t(blockIdx.y) * RB;
+  const int rn = (int)std::min<int64_t>(RB, nitems - r0);
+  if (threadIdx.x < rn) {
+    const int64_t it = items[r0 + threadIdx.x];
+    hg[threadIdx.x] = make_geo(coords[2 * it], coords[2 * it + 1]);
+  }
+  __syncthreads();
+  if (x >= cols) return;
+  const int64_t c = col0 + x;
+  const Geo gc = make_geo(coords[2 * c], coords[2 * c + 1]);
+  for (int r = 0; r < rn; ++r) pr[(r0 + r) * ld + x] = ref_pr_d(a, b, ref_dist(hg[r], gc));
+}
+
+// G[slot * g_ld + c - g_col0] = prod_j pr[row(j), c] over the user's history in CSR order (1.0 for
+// an empty history, -1.0 for history POIs), and gmax[slot] = max(gmax[slot], max over the block's
+// candidates) as u64 bits (non-negative doubles order as their bits). One wave per user, 4
+// columns per lane, 4 users per workgroup -- the layout of pair_gather_topk_kernel.
+__global__ void __launch_bounds__(GW * 64)
+prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_t* __restrict__ rowmap,
+                         const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
+                         const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
+                         double* __restrict__ G, int64_t g_ld, int64_t g_col0,
+                         unsigned long long* __restrict__ gmax) {
+  __shared__ uint32_t hm[GW][STRIPE / 32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t slot = int64_t(blockIdx.x) * GW + w;
+  if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
+  const int64_t u = users[slot];
+  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  const int64_t s0 = int64_t(blockIdx.y) * STRIPE;          // this wave's stripe in the block
+  const int64_t x = s0 + int64_t(lane) * CPL;
+  if (lane < STRIPE / 32) hm[w][lane] = 0u;
+  wave_lds_sync();
+  double g[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) g[q] = 1.0;
+  for (int64_t j0 = 0; j0 < hl; j0 += 64) {
+    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    int64_t mine = 0;
+    if (lane < jn) {
+      const int64_t c = indices[hb + j0 + lane];
+      mine = int64_t(rowmap[c]) * ld;
+      const int64_t r = c - col0 - s0;
+      if (r >= 0 && r < STRIPE && r + s0 < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
+    }
+    const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
+    for (int jj = 0; jj < jn; ++jj) {
+      const double* row = pr + bcast64(mlo, mhi, jj) + x;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q)
+        if (x + q < cols) g[q] = __dmul_rn(g[q], row[q]);
+    }
+  }
+  wave_lds_sync();
+  double m = -1.0;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int64_t xr = x + q;
+    if (xr < cols) {
+      const int64_t r = xr - s0;
+      const bool hist = (hm[w][r >> 5] >> (r & 31)) & 1u;
+      const double v = hist ? -1.0 : g[q];
+      G[slot * g_ld + (col0 - g_col0) + xr] = v;
+      m = fmax(m, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if (lane == 0 && m >= 0.0) atomicMax(gmax + slot, (unsigned long long)__double_as_longlong(m));
+}
+
 // keys -> (ids, scores) of the top-k lists; short lists padded with -1 / NaN and counted
 __global__ void topk_keys_finish_kernel(const unsigned long long* __restrict__ keys,
                                         const int32_t* __restrict__ kcount, int32_t n, int k,
@@ -686,6 +774,48 @@ int32_t nais_pair_gather_topk_l2(const float* table, int64_t chunk_stride, int64
     if (rc) return rc;
   }
   return NAIS_OK;
+}
+
+int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int64_t* items,
+                              int64_t num_items, int64_t col0, int64_t cols, double a, double b,
+                              double* pr, int64_t ld, void* stream) {
+  if (num_pois <= 0 || num_items < 0 || col0 < 0 || cols < 0 || col0 + cols > num_pois || ld < cols)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (num_items == 0 || cols == 0) return NAIS_OK;
+  if (!coords || !items || !pr) return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  const int64_t gy = (num_items + 15) / 16;
+  if (gy > 65535ll * 1024) return nais_internal_fail(NAIS_E_UNSUPPORTED, "too many items");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t y0 = 0; y0 < gy; y0 += 65535) {
+    const int64_t ny = std::min<int64_t>(65535, gy - y0);
+    hipLaunchKernelGGL(prior_pair_table_kernel,
+                       dim3((unsigned)((cols + PRIOR_TAB_THREADS - 1) / PRIOR_TAB_THREADS), (unsigned)ny),
+                       dim3(PRIOR_TAB_THREADS), 0, st, coords, items + y0 * 16,
+                       std::min<int64_t>(num_items - y0 * 16, ny * 16), col0, cols, a, b,
+                       pr + y0 * 16 * ld, ld);
+    const int32_t rc = nais_internal_check_launch("prior_pair_table_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowmap,
+                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                               int32_t num_users, int64_t col0, int64_t cols, double* g, int64_t g_ld,
+                               int64_t g_col0, uint64_t* gmax_bits, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || col0 < g_col0 || g_ld < col0 - g_col0 + cols)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (num_users == 0 || cols == 0) return NAIS_OK;
+  if (!pr || !rowmap || !indptr || !indices || !users || !g || !gmax_bits)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  const int64_t stripes = (cols + STRIPE - 1) / STRIPE;
+  if (stripes > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "cols > 65535 * 256");
+  hipLaunchKernelGGL(prior_pair_gather_kernel,
+                     dim3((unsigned)((num_users + GW - 1) / GW), (unsigned)stripes), dim3(GW * 64), 0,
+                     reinterpret_cast<hipStream_t>(stream), pr, ld, rowmap, indptr, indices, users,
+                     num_users, col0, cols, g, g_ld, g_col0,
+                     reinterpret_cast<unsigned long long*>(gmax_bits));
+  return nais_internal_check_launch("prior_pair_gather_kernel");
 }
 
 int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,

@@ -68,7 +68,8 @@ def test_distance_histogram_and_fit():
     np.testing.assert_allclose([G.a, G.b], z["fit_ab"], rtol=1e-12)
 
 
-def test_score_topk_with_prior_blend():
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
+def test_score_topk_with_prior_blend(strategy):
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
     from poi_recommendation_models_amd.model import NAIS_basic
     z = load_golden("catalog_basic.npz")
@@ -83,7 +84,7 @@ def test_score_topk_with_prior_blend():
     a, b, alpha = 0.052, -1.37, 0.2
     for prec in ("fp32", "fp16x6", "fp16x3"):
         m.precision = prec
-        ids, sc = score_topk(m, csr, range(8), 50, prior=(a, b, alpha, co))
+        ids, sc = score_topk(m, csr, range(8), 50, prior=(a, b, alpha, co), strategy=strategy)
         ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
         for u in range(8):
             hist = z["indices"][z["indptr"][u]:z["indptr"][u + 1]]
@@ -95,3 +96,44 @@ def test_score_topk_with_prior_blend():
             assert_topk_equivalent(rid, rsc, ids[u], sc[u], tie_ulps=8,   # blended f64 prior: ill-conditioned dist(), 8 ulps
                                   
                                    lookup=dict(zip(cand.tolist(), blended.tolist())))
+
+
+def test_pair_prior_gather_equals_prior_rows_bits():
+    """The pairs route's G (nais_pair_prior_table + nais_pair_prior_gather, several column blocks)
+    is bit-identical to nais_powerlaw_prior's rows (the direct route), and so is the per-user max."""
+    from poi_recommendation_models_amd import _capi
+    from poi_recommendation_models_amd.catalog import DeviceCSR, prior_rows
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    data = make_checkins(40, 1500, 60, seed=8)
+    P, U = data.num_pois, data.num_users
+    a, b = 0.052, -1.37
+    dev = torch.device(DEV)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
+    ref, ref_max = prior_rows(csr, range(U), a, b, data.place_coords, dev)
+    lib = _capi.load()
+    users = torch.arange(U, dtype=torch.int32, device=dev)
+    rowmap = torch.empty(P, dtype=torch.int32, device=dev)
+    items = torch.empty(P, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(lib.nais_pair_rows_workspace_size(P), dtype=torch.uint8, device=dev)
+    st = _capi.stream_handle(dev)
+    _capi.check(lib.nais_pair_rows(csr.indptr.data_ptr(), csr.indices.data_ptr(), users.data_ptr(), U, P,
+                                   rowmap.data_ptr(), items.data_ptr(), cnt.data_ptr(), ws.data_ptr(),
+                                   ws.numel(), st), "nais_pair_rows")
+    J = int(cnt.item())
+    co = torch.as_tensor(data.place_coords, dtype=torch.float64, device=dev)
+    W = 384                                             # blocks of 384 columns, the last one partial
+    pr = torch.empty(J, W, dtype=torch.float64, device=dev)
+    G = torch.empty(U, P, dtype=torch.float64, device=dev)
+    gmax = torch.zeros(U, dtype=torch.int64, device=dev)
+    for c0 in range(0, P, W):
+        w = min(W, P - c0)
+        _capi.check(lib.nais_pair_prior_table(co.data_ptr(), P, items.data_ptr(), J, c0, w, a, b,
+                                              pr.data_ptr(), W, st), "nais_pair_prior_table")
+        _capi.check(lib.nais_pair_prior_gather(pr.data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                                               csr.indices.data_ptr(), users.data_ptr(), U, c0, w,
+                                               G.data_ptr(), P, 0, gmax.data_ptr(), st),
+                    "nais_pair_prior_gather")
+    torch.cuda.synchronize()
+    assert torch.equal(G.view(torch.int64), ref.view(torch.int64))
+    assert torch.equal(gmax, ref_max.view(torch.int64))
