@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Copy a gpu_profile.sh run of the pairs-strategy bench into profiles/<round>/pairs/ and record the
 gather kernel's HBM traffic per launch in profiles/traffic.json ("pairs_gather").
-usage: summarize_pairs_profile.py <prof_dir> <out_dir> <num_users> <num_pois> <world> <block_cols>"""
+usage: summarize_pairs_profile.py <prof_dir> <out_dir> <num_users> <num_pois> <world> <block_cols> [precision]"""
 import csv
 import json
 import os
@@ -10,6 +10,7 @@ import sys
 
 src, dst, users, P, world = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
 block_cols = int(sys.argv[6])
+precision = sys.argv[7] if len(sys.argv) > 7 else "fp16x6"
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
 rows = []
@@ -27,7 +28,7 @@ with open(os.path.join(dst, "pmc_summary.csv"), "w", newline="") as fh:
     w.writerows(rows)
 out = {}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
-                 ("catalog", "pairs_table")):
+                 ("catalog", "pairs_table_" + precision)):
     sel = [r for r in rows if tag in r["kernel"]]
     f = [r["value_kb"] for r in sel if r["counter"] == "FETCH_SIZE"]
     wr = [r["value_kb"] for r in sel if r["counter"] == "WRITE_SIZE"]
@@ -35,7 +36,7 @@ for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel
         continue
     fetch, write = sum(f) / len(f), sum(wr) / len(wr)
     out[key] = {"kernel": sel[0]["kernel"], "num_users": users, "num_pois": P, "world": world,
-                "block_cols": block_cols,
+                "block_cols": block_cols, "precision": precision,
                 "dispatches": len(f), "fetch_size_kb": fetch, "write_size_kb": write,
                 "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
                 "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over the "
