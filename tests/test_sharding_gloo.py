@@ -182,3 +182,30 @@ def test_validation_autoroutes_world2():
         assert calls == [U], calls                          # went through the distributed path
         np.testing.assert_allclose(got, z["trained/metrics"], atol=2.0 / U)
     np.testing.assert_array_equal(res[0][2], res[1][2])     # the same 6-tuple on every rank
+
+
+def test_column_blocks_and_min_block_candidates_edges():
+    """P % world != 0 (narrow last block) and worlds with empty blocks. The guard counts
+    each user's candidates inside every rank's real block; distributed_plan falls back to user
+    sharding whenever one block holds fewer than k."""
+    import scipy.sparse as sp
+    from poi_recommendation_models_amd.catalog import DeviceCSR
+    from poi_recommendation_models_amd.sharding import column_blocks, distributed_plan, min_block_candidates
+    blocks = column_blocks(1001, 8)                     # S = 126: last block [882, 1001) = 119 wide
+    assert blocks[0] == (0, 126) and blocks[-1] == (882, 1001)
+    assert sum(c1 - c0 for c0, c1 in blocks) == 1001
+    empty = column_blocks(10, 8)                        # S = 2: ranks 5..7 own nothing
+    assert empty[5:] == [(10, 10)] * 3 and sum(c1 - c0 for c0, c1 in empty) == 10
+    # user 0: 76 history POIs all inside the last block -> 119 - 76 = 43 candidates there
+    hist = [np.arange(882, 958), np.arange(0, 10)]
+    indptr = np.array([0, 76, 86])
+    X = sp.csr_matrix((np.ones(86), np.concatenate(hist), indptr), shape=(2, 1001))
+    csr = DeviceCSR(X, torch.device("cpu"))
+    assert min_block_candidates(csr, [0, 1], 1001, 8) == 43
+    assert min_block_candidates(csr, [1], 1001, 8) == 116   # user 1: block 0 holds 126 - 10
+    assert distributed_plan(csr, 2, 1001, 50, 8) == "users"   # 43 < k: user sharding
+    assert min_block_candidates(csr, [1], 1001, 1) == 1001 - 10          # world 1: the whole catalog
+    X2 = sp.csr_matrix((np.ones(2), np.array([0, 1]), np.array([0, 1, 2])), shape=(2, 10))
+    csr2 = DeviceCSR(X2, torch.device("cpu"))
+    assert min_block_candidates(csr2, [0, 1], 10, 8) == 0    # empty blocks have no candidates
+    assert distributed_plan(csr2, 2, 10, 1, 8) == "users"
