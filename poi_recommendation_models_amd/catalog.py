@@ -252,7 +252,8 @@ _masked: dict = {}
 
 
 def auto_table_cus(model, J, NC, entries, ncu):
-    """CUs for the table stream (the rest gather), in whole XCDs (ncu / 8), from a cost model fitted
+    """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
+    leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/): tables at ~1.1e15 f16 FLOP/s (split-fp16) or
     1.3e14 FLOP/s (fp32) on the whole chip, scaling with their CUs; gathers at ~60 GB/s per CU up
     to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 128 of 256,

@@ -138,6 +138,49 @@ __device__ __forceinline__ int64_t bcast64(uint32_t lo, uint32_t hi, int jj) {
 }
 constexpr int STRIPE = 64 * CPL;             // columns per wave
 
+// Rows issued ahead per wave in the gather loops. A plain `#pragma unroll` over a runtime trip
+// count does not unroll here (the loop holds convergent readlanes), which left one row -- 2 KB per
+// wave -- in flight and the gather latency-bound; GU explicit loads per step keep GU rows in flight
+// while the adds stay in history (CSR) order.
+#ifndef NAIS_GATHER_UNROLL
+#define NAIS_GATHER_UNROLL 8
+#endif
+constexpr int GU = NAIS_GATHER_UNROLL;
+
+// Sa += Σ E[row(j), x..x+CPL), Na += Σ ES[...] over the jn (wave-uniform) rows whose offsets the
+// lanes 0..jn-1 hold in (mlo, mhi), in lane order. Full CPL-column vectors only.
+__device__ __forceinline__ void gather_rows_full(const float* __restrict__ E, const float* __restrict__ ES,
+                                                 uint32_t mlo, uint32_t mhi, int jn, int64_t x,
+                                                 float (&Sa)[CPL], float (&Na)[CPL]) {
+  int jj = 0;
+  for (; jj + GU <= jn; jj += GU) {
+    nfv e[GU], t[GU];
+#pragma unroll
+    for (int g = 0; g < GU; ++g) {
+      const int64_t o = bcast64(mlo, mhi, jj + g) + x;
+      e[g] = loadv(E + o);
+      t[g] = loadv(ES + o);
+    }
+#pragma unroll
+    for (int g = 0; g < GU; ++g)
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) {
+        Sa[q] += e[g][q];
+        Na[q] += t[g][q];
+      }
+  }
+  for (; jj < jn; ++jj) {
+    const int64_t o = bcast64(mlo, mhi, jj) + x;
+    const nfv e = loadv(E + o);
+    const nfv t = loadv(ES + o);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      Sa[q] += e[q];
+      Na[q] += t[q];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(GW * 64)
 pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, int64_t ld,
                    const int32_t* __restrict__ rowmap, const int64_t* __restrict__ indptr,
@@ -145,7 +188,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
                    int32_t nusers, int64_t col0, int64_t cols, float beta,
                    float* __restrict__ scores, int64_t score_ld, int64_t score_col0,
                    int32_t* __restrict__ nan_count) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar user loads
   const int64_t slot = int64_t(blockIdx.x) * GW + w;
   if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
   const int64_t u = users[slot];
@@ -156,22 +199,12 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
 #pragma unroll
   for (int q = 0; q < CPL; ++q) Sa[q] = Na[q] = 0.f;
   for (int64_t j0 = 0; j0 < hl; j0 += 64) {
-    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
     // row offsets of 64 history items, one per lane, broadcast with readlane below
     const int64_t mine = lane < jn ? int64_t(rowmap[indices[hb + j0 + lane]]) * ld : 0;
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
     if (full) {
-#pragma unroll 8
-      for (int jj = 0; jj < jn; ++jj) {
-        const int64_t o = bcast64(mlo, mhi, jj) + x;
-        const nfv e = loadv(E + o);
-        const nfv t = loadv(ES + o);
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-          Sa[q] += e[q];
-          Na[q] += t[q];
-        }
-      }
+      gather_rows_full(E, ES, mlo, mhi, jn, x, Sa, Na);
     } else {
       for (int jj = 0; jj < jn; ++jj) {
         const int64_t o = bcast64(mlo, mhi, jj) + x;
@@ -247,7 +280,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
                         int32_t* __restrict__ nan_count) {
   __shared__ unsigned long long lk[GW][TK_LDS];
   __shared__ uint32_t hm[GW][STRIPE / 32];   // history POIs of this stripe, one bit per column
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t slot = int64_t(blockIdx.x) * GW + w;
   if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
   const int64_t u = users[slot];
@@ -260,7 +293,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
 #pragma unroll
   for (int q = 0; q < CPL; ++q) Sa[q] = Na[q] = 0.f;
   for (int64_t j0 = 0; j0 < hl; j0 += 64) {
-    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
     int64_t mine = 0;
     if (lane < jn) {
       const int64_t c = indices[hb + j0 + lane];
@@ -270,17 +303,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
     }
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
     if (full) {
-#pragma unroll 8
-      for (int jj = 0; jj < jn; ++jj) {
-        const int64_t o = bcast64(mlo, mhi, jj) + x;
-        const nfv e = loadv(E + o);
-        const nfv t = loadv(ES + o);
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-          Sa[q] += e[q];
-          Na[q] += t[q];
-        }
-      }
+      gather_rows_full(E, ES, mlo, mhi, jn, x, Sa, Na);
     } else {
       for (int jj = 0; jj < jn; ++jj) {
         const int64_t o = bcast64(mlo, mhi, jj) + x;
