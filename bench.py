@@ -654,8 +654,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "world_size": world,
             "backend": (a.backend if world > 1 else None),
             "config": {
-                "workload": "config4 Gowalla-scale: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic "
-                            "score + top-%d; one step = every user's whole catalog" % (a.num_users, P, D, K),
+                "workload": "%s: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic score + top-%d; "
+                            "one step = every user's whole catalog"
+                            % ("config4 Gowalla-scale" if a.config == 4 else "config5 stress", a.num_users, P, D, K),
                 "model": "NAIS_basic", "strategy": "pairs", "precision": a.precision,
                 "num_users": a.num_users, "num_pois": P,
                 "table_cus": table["cus"], "cu_layout": catalog.PAIR_CU_LAYOUT,
