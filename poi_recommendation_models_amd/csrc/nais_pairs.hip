@@ -35,6 +35,7 @@ namespace {
 #endif
 constexpr int CPL = NAIS_GATHER_CPL;
 typedef float nfv __attribute__((ext_vector_type(CPL)));
+typedef double ndv __attribute__((ext_vector_type(CPL)));
 
 #ifndef NAIS_GATHER_NT
 #define NAIS_GATHER_NT 0   // 1: non-temporal table loads (slower: the Infinity Cache then holds nothing)
@@ -622,13 +623,14 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int64_t s0 = int64_t(blockIdx.y) * STRIPE;          // this wave's stripe in the block
   const int64_t x = s0 + int64_t(lane) * CPL;
+  const bool full = x + CPL <= cols;
   if (lane < STRIPE / 32) hm[w][lane] = 0u;
   wave_lds_sync();
   double g[CPL];
 #pragma unroll
   for (int q = 0; q < CPL; ++q) g[q] = 1.0;
   for (int64_t j0 = 0; j0 < hl; j0 += 64) {
-    const int jn = (int)std::min<int64_t>(64, hl - j0);
+    const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
     int64_t mine = 0;
     if (lane < jn) {
       const int64_t c = indices[hb + j0 + lane];
@@ -637,7 +639,20 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
       if (r >= 0 && r < STRIPE && r + s0 < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
     }
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
-    for (int jj = 0; jj < jn; ++jj) {
+    int jj = 0;
+    if (full) {   // GU rows' loads in flight (as gather_rows_full), products still in CSR order
+      for (; jj + GU <= jn; jj += GU) {
+        ndv rv[GU];
+#pragma unroll
+        for (int u2 = 0; u2 < GU; ++u2)
+          rv[u2] = *reinterpret_cast<const ndv*>(pr + bcast64(mlo, mhi, jj + u2) + x);
+#pragma unroll
+        for (int u2 = 0; u2 < GU; ++u2)
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) g[q] = __dmul_rn(g[q], rv[u2][q]);
+      }
+    }
+    for (; jj < jn; ++jj) {
       const double* row = pr + bcast64(mlo, mhi, jj) + x;
 #pragma unroll
       for (int q = 0; q < CPL; ++q)
