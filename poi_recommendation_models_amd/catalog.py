@@ -251,21 +251,26 @@ PAIR_L2_WAVES_PER_CU = int(os.environ.get("NAIS_PAIR_L2_WAVES_PER_CU", "20"))
 _masked: dict = {}
 
 
-def auto_table_cus(model, J, NC, entries, ncu):
+def auto_table_cus(model, J, NC, entries, ncu, prior=False):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/): tables at ~1.1e15 f16 FLOP/s (split-fp16) or
     1.3e14 FLOP/s (fp32) on the whole chip, scaling with their CUs; gathers at ~60 GB/s per CU up
-    to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 128 of 256,
-    config 5: 224)."""
+    to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 160 of 256
+    under fp16x6, config 5: 224). With the power-law prior the table stream also builds the float64
+    pr_d table (~1.4e-11 s per pair on the whole chip, profiles/r2/legs_s4) and the gather stream
+    reads it too (8 more bytes per history entry and column)."""
     H, din = model.attn_layer1.weight.shape
     prec = getattr(model, "precision", "fp16x6")
     products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
     t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else 1.1e15)
     gbytes = entries * NC * 8.0
+    if prior:
+        t_tab += J * NC * 1.4e-11
+        gbytes *= 2
     xcd = max(1, ncu // 8)
     best, best_t = ncu // 2, None
-    for n in range(ncu // 2, ncu - xcd + 1, xcd):
+    for n in range(ncu // 4, ncu - xcd + 1, xcd):
         t = max(t_tab * ncu / n, gbytes / min(7.5e12, (ncu - n) * 60e9))
         if best_t is None or t < best_t:
             best, best_t = n, t
@@ -457,7 +462,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             W = int(min(NC, max(256, W // 256 * 256)))
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            table_cus = (auto_table_cus(model, J, NC, entries, ncu) if PAIR_TABLE_CUS < 0
+            table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None) if PAIR_TABLE_CUS < 0
                          else PAIR_TABLE_CUS)
             if events is not None:
                 events.append(("table_cus", None, None, table_cus))

@@ -60,7 +60,10 @@ constexpr int JC = 64;                      // history rows staged in LDS per ch
 constexpr int TOPK_THREADS = 1024;
 constexpr int MAX_K = 1024;
 constexpr int MAX_BATCH_USERS = 512;        // users scored per catalog launch
-constexpr int PAIR_GROUP_ITEMS = 128;       // item rows per workgroup in pair-table mode
+#ifndef NAIS_PAIR_GROUP_ITEMS
+#define NAIS_PAIR_GROUP_ITEMS 128
+#endif
+constexpr int PAIR_GROUP_ITEMS = NAIS_PAIR_GROUP_ITEMS;   // item rows per workgroup in pair-table mode
 
 struct DevParams {
   const float* eh;
@@ -1707,40 +1710,53 @@ __device__ __forceinline__ double unord_f64(unsigned long long o) {
   return __longlong_as_double((long long)u);
 }
 
-// top-k over the f64 blended scores: radix select on the 64-bit ordered score (8 passes), then
-// on ~id among the scores equal to the threshold (4 passes), collect, bitonic sort by (score, ~id).
+// top-k over the f64 blended scores: radix select on the 64-bit ordered score, MSB-first 8-bit
+// digits, stopping as soon as the candidates at or above the selected prefix fit the collect
+// buffer (usually after 2 digits: the row -- 12 B and one f64 division per candidate -- is read
+// 3 times instead of 13); only when more than BLEND_CAP candidates share the whole 64-bit score
+// does it go on to the ~id digits among the scores equal to the threshold (4 passes). Then
+// collect and bitonic-sort by (score, ~id).
+constexpr int BLEND_CAP = 4096;
 __global__ void __launch_bounds__(TOPK_THREADS)
 topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const double* __restrict__ G,
                   int64_t g_ld, const unsigned long long* __restrict__ gmax, int64_t P, int k,
                   float om_alpha_f, double alpha, int32_t* __restrict__ out_ids,
                   float* __restrict__ out_scores, int32_t* __restrict__ short_count) {
   __shared__ uint32_t hist[256];
-  __shared__ unsigned long long bs[MAX_K];
-  __shared__ uint32_t bi[MAX_K];
-  __shared__ uint32_t sh_bin, sh_above, sh_total, sh_cnt;
+  __shared__ unsigned long long bs[BLEND_CAP];
+  __shared__ uint32_t bi[BLEND_CAP];
+  __shared__ uint32_t sh_bin, sh_above, sh_binc, sh_total, sh_cnt;
+  static_assert(BLEND_CAP >= MAX_K, "the id passes collect exactly k keys");
   const float* s = scores + (int64_t)blockIdx.x * score_ld;
   const double* g = G + (int64_t)blockIdx.x * g_ld;
   const double gm = __longlong_as_double((long long)gmax[blockIdx.x]);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned long long prefix = 0, mask = 0;       // over the score key
   uint32_t iprefix = 0, imask = 0;               // over ~id, among score == threshold
-  uint32_t rem = (uint32_t)k;
+  uint32_t rem = (uint32_t)k, above_total = 0, n_collect = 0;
+  bool early = false;                            // stopped on a score digit: collect key >= prefix
   int kk = k;
   for (int pass = 0; pass < 12; ++pass) {
     const bool idpass = pass >= 8;
     const int shift = idpass ? 24 - 8 * (pass - 8) : 56 - 8 * pass;
     if (tid < 256) hist[tid] = 0;
     __syncthreads();
-    for (int64_t c = tid; c < P; c += TOPK_THREADS) {
-      double v;
-      if (!blended(s, g, gm, om_alpha_f, alpha, c, v)) continue;
+    for (int64_t c0 = 0; c0 < P; c0 += TOPK_THREADS) {   // block-uniform trip count (ballots)
+      const int64_t c = c0 + tid;
+      double v = 0.0;
+      const bool ok = c < P && blended(s, g, gm, om_alpha_f, alpha, c, v);
       const unsigned long long key = ord_f64(v);
+      bool pred;
+      uint32_t bin;
       if (!idpass) {
-        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-      } else if (key == prefix) {
+        pred = ok && (key & mask) == prefix;
+        bin = (uint32_t)(key >> shift) & 255u;
+      } else {
         const uint32_t ik = 0xFFFFFFFFu - (uint32_t)c;
-        if ((ik & imask) == iprefix) atomicAdd(&hist[(ik >> shift) & 255], 1u);
+        pred = ok && key == prefix && (ik & imask) == iprefix;
+        bin = (ik >> shift) & 255u;
       }
+      topk_hist_add(hist, pred, bin);
     }
     __syncthreads();
     if (wave == 0) {
@@ -1761,14 +1777,16 @@ topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const doub
       if (need > 0 && excl < need && incl >= need) {
         uint32_t cum = excl;
         int bsel;
-        if (cum + c0 >= need) bsel = base;
-        else if ((cum += c0) + c1 >= need) bsel = base - 1;
-        else if ((cum += c1) + c2 >= need) bsel = base - 2;
-        else { cum += c2; bsel = base - 3; }
+        uint32_t bc;
+        if (cum + c0 >= need) { bsel = base; bc = c0; }
+        else if ((cum += c0) + c1 >= need) { bsel = base - 1; bc = c1; }
+        else if ((cum += c1) + c2 >= need) { bsel = base - 2; bc = c2; }
+        else { cum += c2; bsel = base - 3; bc = c3; }
         sh_bin = (uint32_t)bsel;
         sh_above = cum;
+        sh_binc = bc;
       }
-      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; }
+      if (need == 0 && lane == 0) { sh_bin = 0; sh_above = 0; sh_binc = 0; }
     }
     __syncthreads();
     if (pass == 0) {
@@ -1778,12 +1796,16 @@ topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const doub
     if (!idpass) {
       prefix |= (unsigned long long)sh_bin << shift;
       mask |= 255ull << shift;
+      above_total += sh_above;
+      n_collect = above_total + sh_binc;         // candidates with key >= prefix
     } else {
       iprefix |= sh_bin << shift;
       imask |= 255u << shift;
     }
     rem -= sh_above;
     __syncthreads();
+    if (kk == 0) break;                                            // block-uniform
+    if (!idpass && n_collect <= (uint32_t)BLEND_CAP) { early = true; break; }
   }
   if (tid == 0) sh_cnt = 0;
   __syncthreads();
@@ -1793,9 +1815,9 @@ topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const doub
       if (!blended(s, g, gm, om_alpha_f, alpha, c, v)) continue;
       const unsigned long long key = ord_f64(v);
       const uint32_t ik = 0xFFFFFFFFu - (uint32_t)c;
-      if (key > prefix || (key == prefix && ik >= iprefix)) {
+      if (early ? key >= prefix : (key > prefix || (key == prefix && ik >= iprefix))) {
         const uint32_t pos = atomicAdd(&sh_cnt, 1u);
-        if (pos < (uint32_t)MAX_K) {
+        if (pos < (uint32_t)BLEND_CAP) {
           bs[pos] = key;
           bi[pos] = ik;
         }
@@ -1803,13 +1825,13 @@ topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const doub
     }
   }
   __syncthreads();
+  const int n = kk == 0 ? 0 : (early ? (int)n_collect : kk);
   int n2 = 1;
-  while (n2 < k) n2 <<= 1;
-  for (int i = tid; i < n2; i += TOPK_THREADS)
-    if (i >= kk) {
-      bs[i] = 0ull;
-      bi[i] = 0u;
-    }
+  while (n2 < n || n2 < k) n2 <<= 1;
+  for (int i = n + tid; i < n2; i += TOPK_THREADS) {   // keys of real candidates are > 0
+    bs[i] = 0ull;
+    bi[i] = 0u;
+  }
   __syncthreads();
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {

@@ -1,0 +1,35 @@
+"""CPU test of the pairs route's table / gather CU split (catalog.auto_table_cus): the splits the
+measured A/Bs picked (CU split) and the shader-engine granularity."""
+import types
+
+import pytest
+import torch
+
+from poi_recommendation_models_amd.catalog import auto_table_cus
+
+
+def _model(d, h, precision):
+    return types.SimpleNamespace(attn_layer1=types.SimpleNamespace(weight=torch.empty(h, d)),
+                                 precision=precision)
+
+
+@pytest.mark.parametrize("precision,prior,want", [
+    ("fp16x6", False, 160),   # config 4, the bench default (profiles/r2: 160 / 96 best measured)
+    ("fp16x3", False, 128),   # round 1's split
+    ("fp16x6", True, 128),    # the prior doubles the gathered bytes
+])
+def test_config4_splits(precision, prior, want):
+    assert auto_table_cus(_model(64, 64, precision), 100_000, 100_000, 5_030_351, 256, prior) == want
+
+
+def test_config5_split_is_table_heavy():
+    # one rank's column shard of the 8-GPU job: 1M distinct history POIs x 125k columns
+    assert auto_table_cus(_model(128, 128, "fp16x6"), 1_000_000, 125_000, 20_076_322, 256) == 224
+
+
+@pytest.mark.parametrize("ncu", [64, 128, 256, 304])
+def test_split_in_shader_engine_steps(ncu):
+    for prior in (False, True):
+        n = auto_table_cus(_model(64, 64, "fp16x6"), 50_000, 60_000, 1_000_000, ncu, prior)
+        step = max(1, ncu // 8)
+        assert n % step == 0 and ncu // 4 <= n <= ncu - step

@@ -111,3 +111,76 @@ def test_topk_rows_small_p():
     rng = np.random.default_rng(11)
     for P in (1, 2, 5, 63, 64, 65, 4097):
         _check(_rows("uniform", 3, P, rng), min(50, P))
+
+
+# ---- nais_topk_blend_rows (run.py:537-539 with normalize run.py:55-59): the f64 blended key ----
+def _ref_blend_topk(s, g, gm, alpha, k):
+    """The kernel's total order on f64(f32((1 - alpha) * s)) + alpha * (g / gm): candidates s >= 0
+    (or NaN), NaN first, then blended desc, then id asc; scores reported as f32."""
+    c = np.nonzero(~(s < 0))[0]
+    t = (s[c] * np.float32(1.0 - alpha)).astype(np.float64)
+    gn = g[c] / gm if gm != 0.0 else g[c]
+    v = t + alpha * gn
+    nan = np.isnan(v)
+    o = np.lexsort((c, -np.where(nan, 0, v), ~nan))[:k]
+    ids = np.full(k, -1, np.int64)
+    sc = np.full(k, np.nan, np.float32)
+    ids[:len(o)] = c[o]
+    sc[:len(o)] = v[o].astype(np.float32)
+    return ids, sc, len(c) < k
+
+
+def _check_blend(s, g, k, alpha=0.2):
+    from poi_recommendation_models_amd import _capi
+    n, P = s.shape
+    gmv = np.array([max([x for x in g[r][~(s[r] < 0)]] + [0.0]) for r in range(n)], np.float64)
+    ts, tg = torch.from_numpy(s).to(DEV), torch.from_numpy(g).to(DEV)
+    tm = torch.from_numpy(gmv.view(np.int64)).to(DEV)
+    ids = torch.empty(n, k, dtype=torch.int32, device=DEV)
+    sc = torch.empty(n, k, dtype=torch.float32, device=DEV)
+    short = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _capi.check(_capi.load().nais_topk_blend_rows(
+        ts.data_ptr(), P, tg.data_ptr(), P, tm.data_ptr(), P, n, k, alpha, ids.data_ptr(),
+        sc.data_ptr(), short.data_ptr(), _capi.stream_handle(torch.device(DEV))), "nais_topk_blend_rows")
+    torch.cuda.synchronize()
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    nshort = 0
+    for r in range(n):
+        rid, rsc, sh = _ref_blend_topk(s[r], g[r], gmv[r], alpha, k)
+        nshort += sh
+        np.testing.assert_array_equal(ids[r], rid, err_msg=f"row {r}")
+        ok = ~np.isnan(rsc)
+        np.testing.assert_array_equal(sc[r].view(np.int32)[ok], rsc.view(np.int32)[ok])
+        assert np.all(np.isnan(sc[r][~ok]))
+    assert int(short.item()) == nshort
+
+
+@pytest.mark.parametrize("kind", ["sigmoid", "quantized", "equal", "narrow"])
+@pytest.mark.parametrize("k", [1, 50, 1024])
+def test_topk_blend_rows_kinds(kind, k):
+    """Early exit after a few score digits (sigmoid), ties straddling rank k (quantized), one
+    blended value for every candidate (equal: > 4,096 equal keys force the ~id digits), a wide
+    top bin (narrow)."""
+    rng = np.random.default_rng(zlib.crc32(f"blend/{kind}/{k}".encode()))
+    s = _rows(kind, 4, 30011, rng)
+    if kind == "equal":
+        g = np.full(s.shape, 0.25, np.float64)
+    elif kind == "quantized":
+        g = np.round(rng.random(s.shape) * 50) / 50
+    else:
+        g = rng.random(s.shape) ** 8          # a power-law-like spread of products
+    g[s < 0] = -1.0
+    _check_blend(s, g, k)
+
+
+def test_topk_blend_rows_nan_zero_max_and_short():
+    rng = np.random.default_rng(19)
+    s = _rows("uniform", 4, 5000, rng)
+    g = rng.random(s.shape)
+    s[0, [7, 123]] = np.nan                   # NaN scores rank first
+    g[1, :] = 0.0                             # every product underflowed: gmax 0, no normalisation
+    s[2, :] = -1.0
+    s[2, [4, 40, 400]] = [0.3, 0.3, 0.1]      # 3 candidates < k
+    s[3, 4100:] = -1.0
+    g[s < 0] = -1.0
+    _check_blend(s, g, 50)
