@@ -47,6 +47,13 @@ _csr_cache: dict = {}
 _ws_cache: dict = {}
 
 
+def _user_array(users):
+    """User ids as int64 numpy (an ndarray or range without a per-element Python round trip)."""
+    if isinstance(users, (np.ndarray, range)):
+        return np.asarray(users, dtype=np.int64).reshape(-1)
+    return np.asarray(list(users), dtype=np.int64)
+
+
 def device_csr(train_matrix, device) -> DeviceCSR:
     if isinstance(train_matrix, DeviceCSR):
         return train_matrix
@@ -102,7 +109,7 @@ def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlo
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model._item_tables()[0].shape[0]
-    users = np.asarray(list(users), dtype=np.int64)
+    users = _user_array(users)
     u_dev = torch.from_numpy(users.astype(np.int32)).to(dev)
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
     out = torch.empty(len(users), P, dtype=torch.float32, device=dev)
@@ -169,7 +176,7 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     P = model._item_tables()[0].shape[0]
     if csr.shape[1] != P:
         raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
-    users = np.asarray(list(users), dtype=np.int64)
+    users = _user_array(users)
     if len(users) == 0:
         return (torch.empty(0, k, dtype=torch.int64, device=dev),
                 torch.empty(0, k, dtype=torch.float32, device=dev))
@@ -336,7 +343,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         raise ValueError(f"train_matrix has {csr.shape[1]} POIs, model has {P}")
     c0_all, c1_all = cols if cols is not None else (0, P)
     NC = c1_all - c0_all
-    users = np.asarray(list(users), dtype=np.int64)
+    users = _user_array(users)
     n = len(users)
     if n == 0 or NC <= 0:
         return None
@@ -569,7 +576,7 @@ def prior_rows(train_matrix, users, a, b, coords, device):
     dev = torch.device(device)
     csr = device_csr(train_matrix, dev)
     P = csr.shape[1]
-    users = np.asarray(list(users), dtype=np.int64)
+    users = _user_array(users)
     u_dev = torch.from_numpy(users.astype(np.int32)).to(dev)
     cor = torch.as_tensor(np.ascontiguousarray(coords, dtype=np.float64)).to(dev)
     out = torch.empty(len(users), P, dtype=torch.float64, device=dev)

@@ -83,13 +83,22 @@ def column_blocks(num_pois, world):
     return [(min(r * S, num_pois), min((r + 1) * S, num_pois)) for r in range(world)]
 
 
+_mbc_cache = {}
+
+
 def min_block_candidates(csr, users, num_pois, world):
     """min over (listed user, rank) of the candidates the user has inside the rank's column block:
     the block's width minus the user's history POIs that fall in it. The column-sharded merge
-    needs >= k of them everywhere (a short block list would be padded with id -1)."""
-    users = np.asarray(list(users), dtype=np.int64)
+    needs >= k of them everywhere (a short block list would be padded with id -1). Cached per
+    (CSR, users, world): distributed_topk_pairs checks it on every call, and at config 4 the
+    count over 5M history entries costs tens of ms of host time -- a third of an 8-GPU step."""
+    users = np.asarray(users, dtype=np.int64).reshape(-1)
     if len(users) == 0:
         return num_pois
+    key = (id(csr), num_pois, world, len(users), hash(users.tobytes()))
+    hit = _mbc_cache.get(key)
+    if hit is not None and hit[0] is csr:
+        return hit[1]
     blocks = column_blocks(num_pois, world)
     width = np.array([c1 - c0 for c0, c1 in blocks], dtype=np.int64)
     S = (num_pois + world - 1) // world
@@ -98,9 +107,12 @@ def min_block_candidates(csr, users, num_pois, world):
     starts = csr.host_indptr[users]
     pos = np.repeat(starts - np.concatenate([[0], np.cumsum(h)[:-1]]), h) + np.arange(int(h.sum()))
     blk = csr.host_indices[pos] // S
-    inside = np.zeros((len(users), world), dtype=np.int64)
-    np.add.at(inside, (rows, blk), 1)
-    return int((width[None, :] - inside).min())
+    inside = np.bincount(rows * world + blk, minlength=len(users) * world).reshape(len(users), world)
+    out = int((width[None, :] - inside).min())
+    if len(_mbc_cache) > 8:
+        _mbc_cache.clear()
+    _mbc_cache[key] = (csr, out)
+    return out
 
 
 def distributed_plan(csr, num_users, num_pois, k, world, model=None):
@@ -169,7 +181,7 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = csr.shape[1]
-    users = np.asarray(list(users), dtype=np.int64)
+    users = np.asarray(users if isinstance(users, np.ndarray) else list(users), dtype=np.int64)
     n = len(users)
     if world > 1 and min_block_candidates(csr, users, P, world) < k:
         raise ValueError("a column block has fewer than k candidates for some user "
