@@ -631,7 +631,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                                            "coordinates, %s tables" % a.precision)
         del rd
     check = None
-    if world == 1 and emulate == 1 and not a.no_self_check and rank == 0:
+    if emulate == 1 and not a.no_self_check and rank == 0:   # N > 1: the merged top-k
         ids, sc = last["out"]
         check = self_check(p_host, data, [1, 4242 % a.num_users], ids.cpu().numpy(), sc.cpu().numpy(), K)
     if rank == 0:
