@@ -38,6 +38,9 @@ namespace {
 #ifndef NAIS_WAVES
 #define NAIS_WAVES 8
 #endif
+#ifndef NAIS_X3B_NW
+#define NAIS_X3B_NW NAIS_WAVES   // waves per workgroup of the item-side split kernel
+#endif
 #ifndef NAIS_X3B_SCHED
 #define NAIS_X3B_SCHED 0
 #endif
@@ -1046,7 +1049,7 @@ struct CfgB {
 
 // NW = waves per workgroup (2 per SIMD at 8). D, H <= 64 pipeline the epilogue (CfgB::PIPE).
 template <int DH, int HB, int VAR, int NW, int NPC>
-__global__ void __launch_bounds__(NW * 64, 1)
+__global__ void __launch_bounds__(NW * 64, NW >= 8 ? 1 : 8 / NW)   // >= 2 waves per SIMD per CU
 catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                          const int64_t* __restrict__ region_of, const double* __restrict__ coords,
@@ -2103,7 +2106,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     return launch_catalog_x3<DH, HB, VAR, NPC>(d, indptr, indices, users, nb, region_of, coords,
                                                latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
-    constexpr int NW = WAVES;
+    constexpr int NW = NAIS_X3B_NW;   // A/B: 4 = two 4-wave workgroups per CU (barriers decoupled)
     const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW, NPC>::BYTES;
     auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW, NPC>;
     static bool attr_set = false;
