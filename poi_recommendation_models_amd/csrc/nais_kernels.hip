@@ -41,6 +41,9 @@ namespace {
 #ifndef NAIS_X3B_NW
 #define NAIS_X3B_NW NAIS_WAVES   // waves per workgroup of the item-side split kernel
 #endif
+#ifndef NAIS_X3B_DIST
+#define NAIS_X3B_DIST 1   // distance variants on the item-side kernel where it pipelines (D, H <= 64)
+#endif
 #ifndef NAIS_X3B_SCHED
 #define NAIS_X3B_SCHED 0
 #endif
@@ -2099,10 +2102,12 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
-  } else if constexpr (VarT<VAR>::DIST || (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32)) ||
+  } else if constexpr ((VarT<VAR>::DIST && !(NAIS_X3B_DIST && CfgB<DH, HB, true, NAIS_X3B_NW, NPC>::PIPE)) ||
+                       (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32)) ||
                        CfgB<DH, HB, false, WAVES, NPC>::BYTES > kLdsBytes) {
-    // the distance features ride on the per-pair split kernel (also in pair-table mode); so do
-    // shapes whose item ring does not fit the LDS (fp16x6 at D = H = 128: 2 x 96 KiB per item)
+    // the distance features ride on the per-pair split kernel (also in pair-table mode) except on
+    // the pipelined item-side shapes (D, H <= 64), whose step adds them as one exact fp32 MFMA
+    // K-step; so do shapes whose item ring does not fit the LDS (fp16x6 at D = H = 128)
     return launch_catalog_x3<DH, HB, VAR, NPC>(d, indptr, indices, users, nb, region_of, coords,
                                                latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
