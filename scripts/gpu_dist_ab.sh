@@ -1,6 +1,7 @@
 #!/bin/bash
 # Distance variants on the item-side kernel (in-tree) vs the per-pair split kernel
-# (build_ab/nodist.so, -DNAIS_X3B_DIST=0): distance parity tests, then the bench legs of each.
+# (build_ab/nodist.so: python scripts/build_ab.py nodist=-DNAIS_X3B_DIST=0): distance parity tests,
+# then the bench legs of each.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/dist
