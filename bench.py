@@ -55,9 +55,10 @@ DTYPES = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", type=int, default=4, choices=[4, 5],
-                    help="4: 50k users x 100k POIs, d=H=64 (the metric config); 5: stress, 200k users x "
-                         "1M POIs, d=H=128, tables sharded + all-gathered, timed on the first 4096 users")
+    ap.add_argument("--config", type=int, default=4, choices=[2, 4, 5],
+                    help="4: 50k users x 100k POIs, d=H=64 (the metric config); 2: 10k users x 50k POIs, "
+                         "d=H=64, h<=100 (whole job, pairs route); 5: stress, 200k users x 1M POIs, "
+                         "d=H=128, tables sharded + all-gathered, timed on the first 4096 users")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--users-per-step", type=int, default=256)
@@ -171,6 +172,8 @@ def self_launch(a):
 
 def main():
     a = parse()
+    if a.config == 2:
+        a.num_users, a.num_pois, a.dim, a.hidden, a.h_max = 10_000, 50_000, 64, 64, 100
     if a.config == 5:
         a.num_users, a.num_pois, a.dim, a.hidden = 200_000, 1_000_000, 128, 128
         if a.users_per_step == 256:
@@ -247,7 +250,7 @@ def main():
     model.precision = a.precision
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
     hist_len = data.hist_len()
-    strategy = a.strategy if a.strategy != "auto" else ("pairs" if a.config == 4 else "direct")
+    strategy = a.strategy if a.strategy != "auto" else ("direct" if a.config == 5 else "pairs")
     if strategy == "pairs":
         return bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist)
     subset = np.arange(4096) if a.config == 5 else None
@@ -360,7 +363,7 @@ def main():
             cpu = cpu_baseline(p_host, data, np.arange(a.cpu_users), K, a.cpu_seconds)
         out = {
             "metric": "scored (user,POI) pairs/sec full-catalog + top-50, %s POIs"
-                      % ("100k" if a.config == 4 else "1M"),
+                      % {2: "50k", 4: "100k", 5: "1M"}[a.config],
             "value": pairs_total / elapsed,
             "unit": "pairs/s",
             "n_gpus": world,
@@ -373,8 +376,8 @@ def main():
             "dtype": DTYPES[a.precision],
             "data": "synthetic (seeded CSR check-ins, h~U{1..%d}; random-init weights N(0,0.3))" % a.h_max,
             "config": {
-                "workload": ("config4 Gowalla-scale" if a.config == 4 else
-                             "config5 stress (timed on the first 4096 users)") +
+                "workload": {2: "config2 synthetic", 4: "config4 Gowalla-scale"}.get(
+                    a.config, "config5 stress (timed on the first 4096 users)") +
                             ": %d users x %d POIs, d=H=%d, full-catalog NAIS_basic score + top-%d"
                             % (a.num_users, P, D, K),
                 "table_allgather_ms": gather_ms,
@@ -639,7 +642,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(p_host, data, np.arange(a.cpu_users), K, a.cpu_seconds)
         out = {
-            "metric": "scored (user,POI) pairs/sec full-catalog + top-50, 100k POIs",
+            "metric": "scored (user,POI) pairs/sec full-catalog + top-50, %s POIs"
+                      % {2: "50k", 4: "100k", 5: "1M"}[a.config],
             "value": pairs_job * a.steps / elapsed,
             "unit": "pairs/s",
             "n_gpus": world,
@@ -656,7 +660,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "config": {
                 "workload": "%s: %d users x %d POIs, d=H=%d, full-catalog NAIS_basic score + top-%d; "
                             "one step = every user's whole catalog"
-                            % ("config4 Gowalla-scale" if a.config == 4 else "config5 stress", a.num_users, P, D, K),
+                            % ({2: "config2 synthetic", 4: "config4 Gowalla-scale"}.get(a.config, "config5 stress"), a.num_users, P, D, K),
                 "model": "NAIS_basic", "strategy": "pairs", "precision": a.precision,
                 "num_users": a.num_users, "num_pois": P,
                 "table_cus": table["cus"], "cu_layout": catalog.PAIR_CU_LAYOUT,
