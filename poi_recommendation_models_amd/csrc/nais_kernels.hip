@@ -1023,7 +1023,10 @@ struct CfgB {
 #endif
 #endif
   // LDS chunk rows; fp16x6 keeps 32 (the s tile below) even where 64 would fit
-  static constexpr int JCB = (NPC == 3 || 2 * G * IB + 64 * D * 4 > 140 * 1024) ? 32 : 64;
+#ifndef NAIS_X3B_JCB6
+#define NAIS_X3B_JCB6 32   // A/B: 64-row chunks for fp16x6 (needs NAIS_X3B_SMFMA=0: the s tile is 32 rows)
+#endif
+  static constexpr int JCB = (NPC == 3) ? NAIS_X3B_JCB6 : (2 * G * IB + 64 * D * 4 > 140 * 1024 ? 32 : 64);
   static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);  // build entries per thread
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
