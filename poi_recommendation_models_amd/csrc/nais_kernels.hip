@@ -1721,8 +1721,8 @@ __device__ __forceinline__ double unord_f64(unsigned long long o) {
 
 // top-k over the f64 blended scores: radix select on the 64-bit ordered score, MSB-first 8-bit
 // digits, stopping as soon as the candidates at or above the selected prefix fit the collect
-// buffer (usually after 2 digits: the row -- 12 B and one f64 division per candidate -- is read
-// 3 times instead of 13); only when more than BLEND_CAP candidates share the whole 64-bit score
+// buffer (after 2-3 digits for scores spread over (0, 1): the row -- 12 B and one f64 division per
+// candidate -- is read 3-4 times instead of 13); only when more than BLEND_CAP candidates share the whole 64-bit score
 // does it go on to the ~id digits among the scores equal to the threshold (4 passes). Then
 // collect and bitonic-sort by (score, ~id).
 constexpr int BLEND_CAP = 4096;
