@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Copy a gpu_profile.sh run of the pairs-strategy bench into profiles/<round>/pairs/ and record the
-gather kernel's HBM traffic per launch in profiles/traffic.json ("pairs_gather").
+gather kernel's HBM traffic per launch (pmc_by_kernel.csv: per-kernel counter means) in profiles/traffic.json ("pairs_gather").
 usage: summarize_pairs_profile.py <prof_dir> <out_dir> <num_users> <num_pois> <world> <block_cols> [precision]"""
 import csv
 import json
@@ -22,10 +22,16 @@ for sub in ("pmc_fetch", "pmc_write"):
             rows.append({"kernel": name, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
                          "value_kb": float(r["Counter_Value"]), "grid": r["Grid_Size"],
                          "wg": r["Workgroup_Size"], "lds": r["LDS_Block_Size"], "vgpr": r["VGPR_Count"]})
-with open(os.path.join(dst, "pmc_summary.csv"), "w", newline="") as fh:
-    w = csv.DictWriter(fh, fieldnames=list(rows[0].keys()))
-    w.writeheader()
-    w.writerows(rows)
+# one row per (kernel, counter): dispatch count and mean / min / max per dispatch (the per-dispatch
+# rows of a full bench run are ~30k lines)
+agg = {}
+for r in rows:
+    agg.setdefault((r["kernel"], r["counter"]), (r, []))[1].append(r["value_kb"])
+with open(os.path.join(dst, "pmc_by_kernel.csv"), "w", newline="") as fh:
+    w = csv.writer(fh)
+    w.writerow(["kernel", "counter", "dispatches", "mean_kb", "min_kb", "max_kb", "wg", "lds", "vgpr"])
+    for (kern, ctr), (r0, v) in sorted(agg.items()):
+        w.writerow([kern, ctr, len(v), sum(v) / len(v), min(v), max(v), r0["wg"], r0["lds"], r0["vgpr"]])
 out = {}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
                  ("catalog", "pairs_table_" + precision)):
