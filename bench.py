@@ -136,14 +136,18 @@ def cpu_baseline(p, data, users, k, seconds):
                       f"{threads} threads), {pairs} pairs in {dt:.1f} s"}
 
 
-def self_check(p, data, users, ids, sc, k):
+def self_check(p, data, users, ids, sc, k, scorer=None):
     """Oracle check of the timed path's output for a few users (numpy restatement, test
     infrastructure): every returned id's oracle score within 1e-4 of ours, and the returned set
-    equal to the oracle's top-k up to runs of scores within 4 fp32 ulps at the cut."""
+    equal to the oracle's top-k up to runs of scores within 4 fp32 ulps at the cut. `scorer(u)` ->
+    (candidates, oracle scores); default NAIS_basic."""
     from oracle import nais_oracle
+    if scorer is None:
+        def scorer(u):
+            return nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois, chunk=4096)
     out = {"users": [], "max_abs_score_diff": 0.0, "topk_ok": True}
     for u in users:
-        cand, ref = nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois, chunk=4096)
+        cand, ref = scorer(u)
         lut = dict(zip(cand.tolist(), ref.tolist()))
         got = np.array([lut[int(c)] for c in ids[u]])
         out["max_abs_score_diff"] = max(out["max_abs_score_diff"], float(np.max(np.abs(got - sc[u]))))
@@ -420,11 +424,11 @@ def variant_leg(name, job, steps, pairs_job, dev):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
-        job()
+        out = job()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     return {"value": pairs_job * steps / el, "unit": "pairs/s", "steps": steps, "warmup": 1,
-            "ms_per_step": el / steps * 1e3}
+            "ms_per_step": el / steps * 1e3}, out
 
 
 def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
@@ -611,7 +615,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                           "table_peak_tflops": t_l["peak"], "table_cus": t_l["cus"],
                           "gather_ms_per_step": g_l["ms_per_step"]}
         model.precision = a.precision
-        legs["prior"] = variant_leg("prior", lambda: _score_topk_pairs(
+        legs["prior"], _ = variant_leg("prior", lambda: _score_topk_pairs(
             model, csr, users, K, None, None, None, None, force=True,
             prior=(PRIOR_A, PRIOR_B, PRIOR_ALPHA, data.place_coords)), a.leg_steps, pairs_job, dev)
         legs["prior"]["what"] = ("the same job ranked on the power-law-blended score (run.py:537-539): "
@@ -620,15 +624,20 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         from poi_recommendation_models_amd.model import NAIS_region_distance_Embedding
         from poi_recommendation_models_amd.synthetic import init_nais_params as _init
         rd = NAIS_region_distance_Embedding(P, D, H, 0.5, 1024, 1)
-        rd.load_state_dict({k: torch.from_numpy(v) for k, v in
-                            _init(P, D, H, seed=11, emb_std=0.3, bias_std=0.1, variant="region_distance",
-                                  num_regions=1024).items()}, strict=False)
+        p_rd = _init(P, D, H, seed=11, emb_std=0.3, bias_std=0.1, variant="region_distance", num_regions=1024)
+        rd.load_state_dict({k: torch.from_numpy(v) for k, v in p_rd.items()}, strict=False)
         rd = rd.to(dev).eval()
         rd.report_nan = False
         rd.precision = a.precision
-        legs["region_distance"] = variant_leg("region_distance", lambda: _score_topk_pairs(
+        legs["region_distance"], rd_out = variant_leg("region_distance", lambda: _score_topk_pairs(
             rd, csr, users, K, data.region_of, data.place_coords, None, None, force=True),
             a.leg_steps, pairs_job, dev)
+        if not a.no_self_check:   # one user against the numpy restatement of validation.py:69-121
+            from oracle import nais_oracle
+            legs["region_distance"]["self_check"] = self_check(
+                p_rd, data, [1], rd_out[0].cpu().numpy(), rd_out[1].cpu().numpy(), K,
+                scorer=lambda u: nais_oracle.catalog_scores_region_distance(
+                    p_rd, data.history(int(u)), P, data.region_of, data.place_coords))
         legs["region_distance"]["what"] = ("NAIS_region_distance_Embedding (model.py:246-297) on the same "
                                            "users / POIs: [h | region] rows, distance features from the POI "
                                            "coordinates, %s tables" % a.precision)
