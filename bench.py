@@ -76,6 +76,8 @@ def parse():
                     help="CPU baseline sample: the first N users (after a 1-user warm-up)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="cap on the CPU sample's time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather-leg", action="store_true",
+                    help="skip the standalone history-gather leg (nais_gather_rows, 2 GB table)")
     ap.add_argument("--no-self-check", action="store_true",
                     help="skip the oracle check of 2 bench users' top-50 after the timed steps")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -136,16 +138,46 @@ def cpu_baseline(p, data, users, k, seconds):
                       f"{threads} threads), {pairs} pairs in {dt:.1f} s"}
 
 
-def self_check(p, data, users, ids, sc, k, scorer=None):
-    """Oracle check of the timed path's output for a few users (numpy restatement, test
-    infrastructure): every returned id's oracle score within 1e-4 of ours, and the returned set
-    equal to the oracle's top-k up to runs of scores within 4 fp32 ulps at the cut. `scorer(u)` ->
-    (candidates, oracle scores); default NAIS_basic."""
+def torch_scorer(p, data):
+    """(candidates, scores) of one user's whole catalog through oracle/torch_cpu.py (the
+    reference's loop in torch CPU ops, pinned to the reference's outputs by
+    tests/test_torch_cpu_baseline.py) -- ~4x faster than the numpy oracle on the same cores."""
+    from oracle import torch_cpu
+    m = torch_cpu.TorchNAIS(p)
+
+    def scorer(u):
+        rows, cand = torch_cpu.candidates(data.history(int(u)), data.num_pois)
+        with torch.no_grad():
+            ref = torch.cat([m(rows[c:c + 1024], cand[c:c + 1024]) for c in range(0, len(cand), 1024)])
+        return cand.numpy(), ref.numpy()
+    return scorer
+
+
+def numpy_scorer(p, data):
+    from oracle import nais_oracle
+
+    def scorer(u):
+        return nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois, chunk=4096)
+    return scorer
+
+
+def spread_users(hist_len, n):
+    """n users spread over the history lengths: shortest, longest and the quantiles between."""
+    order = np.argsort(hist_len, kind="stable")
+    pos = np.unique(np.round(np.linspace(0, len(order) - 1, n)).astype(np.int64))
+    return [int(u) for u in order[pos]]
+
+
+def self_check(p, data, users, ids, sc, k, scorer=None, oracle_name=None):
+    """Oracle check of the timed path's output for a few users (test infrastructure): every
+    returned id's oracle score within 1e-4 of ours, and the returned set equal to the oracle's
+    top-k up to runs of scores within 4 fp32 ulps at the cut. `scorer(u)` -> (candidates, oracle
+    scores); default NAIS_basic through the numpy oracle."""
     from oracle import nais_oracle
     if scorer is None:
-        def scorer(u):
-            return nais_oracle.catalog_scores_basic(p, data.history(int(u)), data.num_pois, chunk=4096)
-    out = {"users": [], "max_abs_score_diff": 0.0, "topk_ok": True}
+        scorer, oracle_name = numpy_scorer(p, data), "oracle/nais_oracle.py (numpy)"
+    t0 = time.perf_counter()
+    out = {"users": [], "oracle": oracle_name, "max_abs_score_diff": 0.0, "topk_ok": True}
     for u in users:
         cand, ref = scorer(u)
         lut = dict(zip(cand.tolist(), ref.tolist()))
@@ -157,7 +189,92 @@ def self_check(p, data, users, ids, sc, k, scorer=None):
         ok = all(lut[c] >= cut for c in extra) and out["max_abs_score_diff"] <= 1e-4
         out["topk_ok"] = out["topk_ok"] and ok
         out["users"].append(int(u))
+    out["h"] = [int(data.hist_len()[u]) for u in out["users"]]
+    out["seconds"] = round(time.perf_counter() - t0, 1)
     return out
+
+
+def merge_checks(*checks):
+    """One self_check record from several (e.g. the numpy oracle on one user + torch_cpu on 8)."""
+    checks = [c for c in checks if c]
+    return {"users": sum((c["users"] for c in checks), []), "h": sum((c["h"] for c in checks), []),
+            "oracle": " + ".join(f"{c['oracle']} on users {c['users']}" for c in checks),
+            "max_abs_score_diff": max(c["max_abs_score_diff"] for c in checks),
+            "topk_ok": all(c["topk_ok"] for c in checks),
+            "seconds": round(sum(c["seconds"] for c in checks), 1)}
+
+
+def prior_self_check(p, data, user, ids, sc, k, a_, b_, alpha):
+    """The blended ranking of run.py:537-539 for one user: NAIS scores from the numpy oracle,
+    G = powerLaw.predict per candidate (oracle/powerlaw_oracle.py, pure-Python float64),
+    normalize (run.py:55-59), blend -- then the same checks as self_check on the blended f64 scores
+    (relative 1e-6: the reference's libm and the device's differ by ulps in acos / pow)."""
+    from oracle import nais_oracle, powerlaw_oracle
+    t0 = time.perf_counter()
+    hist = data.history(int(user))
+    cand, pred = nais_oracle.catalog_scores_basic(p, hist, data.num_pois, chunk=4096)
+    coords = [tuple(c) for c in np.asarray(data.place_coords, dtype=np.float64).tolist()]
+    G = np.array([powerlaw_oracle.predict(a_, b_, coords, hist, int(c)) for c in cand])
+    G = np.asarray(powerlaw_oracle.normalize(list(G)), dtype=np.float64)
+    ref = powerlaw_oracle.blend(pred, G, alpha)
+    lut = dict(zip(cand.tolist(), ref.tolist()))
+    got = np.array([lut[int(c)] for c in ids[user]])
+    diff = float(np.max(np.abs(got - sc[user].astype(np.float64))))
+    rid, rsc = nais_oracle.topk_ids(cand, ref, k)
+    cut = float(rsc[-1]) * (1 - 1e-6)
+    extra = set(ids[user].tolist()) - set(rid.tolist())
+    ok = all(lut[c] >= cut for c in extra) and diff <= 1e-4
+    return {"users": [int(user)], "h": [len(hist)], "max_abs_score_diff": diff, "topk_ok": ok,
+            "oracle": "oracle/nais_oracle.py + oracle/powerlaw_oracle.py (predict, normalize, blend)",
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
+def gather_rows_leg(dev, lib, traffic_json, rows=4_000_000, dim=128, m=4_000_000, reps=10):
+    """The north star's HBM kernel on its own (nais_gather_rows = model.py:64's embedding gather):
+    a 2 GB table (4M rows x d = 128, past the 256 MB Infinity Cache), 4M rows gathered in random
+    permutation order (each row read once). Algorithmic bytes per launch = m x (8 B index + 4d B
+    row read + 4d B row write); HIP events on the launch stream; frac against the 8 TB/s spec and
+    the 6.29 TB/s measured copy ceiling (MI355X_MICROARCH.md); traffic from the committed
+    FETCH_SIZE / WRITE_SIZE passes (profiles/traffic.json "gather_rows")."""
+    from poi_recommendation_models_amd import _capi
+    g = torch.Generator(device=dev).manual_seed(0)
+    table = torch.randn(rows, dim, device=dev, generator=g)
+    idx = torch.randperm(rows, device=dev, generator=g)[:m].contiguous()
+    out = torch.empty(m, dim, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def launch():
+        _capi.check(lib.nais_gather_rows(table.data_ptr(), rows, dim, idx.data_ptr(), m,
+                                         out.data_ptr(), stream.cuda_stream), "nais_gather_rows")
+    launch()
+    torch.cuda.synchronize(dev)
+    ms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms.append(e0.elapsed_time(e1))
+    ok = bool(torch.equal(out, table.index_select(0, idx)))   # every gathered row, bit-exact
+    algo = m * (8 + 8 * dim)
+    avg = float(np.mean(ms))
+    ach = algo / (avg * 1e-3) / 1e9
+    traffic = None
+    try:
+        e = json.load(open(traffic_json)).get("gather_rows", {})
+        if e.get("rows") == rows and e.get("dim") == dim and e.get("m") == m:
+            traffic = e.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    del table, idx, out
+    torch.cuda.empty_cache()
+    return {"kernel": "gather_rows_kernel (nais_gather_rows)", "bound": "hbm", "unit": "GB/s",
+            "achieved": ach, "peak": HBM_SPEC_GBS, "frac": ach / HBM_SPEC_GBS,
+            "measured_hbm_peak": HBM_MEASURED_GBS, "frac_of_measured_hbm": ach / HBM_MEASURED_GBS,
+            "traffic": traffic, "algorithmic_bytes_per_launch": algo, "avg_launch_ms": avg,
+            "launches": reps, "table_bytes": rows * dim * 4, "rows_gathered": m, "dim": dim,
+            "index_pattern": "random permutation (each row read once)", "rows_bit_exact": ok}
 
 
 def self_launch(a):
@@ -608,16 +725,27 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             a_steps[prec] = a.leg_steps
             el_l, per_l = run(prec, 1, a.leg_steps)
             g_l, t_l = kernels(per_l, prec)
+            leg_check = None
+            if not a.no_self_check:   # 2 users of this leg's last job against the restatement
+                li, ls = (t.cpu().numpy() for t in last["out"])
+                leg_check = self_check(p_host, data, spread_users(hist_len, 2), li, ls, K,
+                                       scorer=torch_scorer(p_host, data),
+                                       oracle_name="oracle/torch_cpu.py")
             legs[prec] = {"precision": DTYPES[prec], "value": pairs_job * a.leg_steps / el_l,
                           "unit": "pairs/s", "steps": a.leg_steps, "warmup": 1,
                           "ms_per_step": el_l / a.leg_steps * 1e3,
                           "table_ms_per_step": t_l["ms_per_step"], "table_tflops": t_l["achieved"],
                           "table_peak_tflops": t_l["peak"], "table_cus": t_l["cus"],
-                          "gather_ms_per_step": g_l["ms_per_step"]}
+                          "gather_ms_per_step": g_l["ms_per_step"], "self_check": leg_check}
         model.precision = a.precision
-        legs["prior"], _ = variant_leg("prior", lambda: _score_topk_pairs(
+        legs["prior"], pr_out = variant_leg("prior", lambda: _score_topk_pairs(
             model, csr, users, K, None, None, None, None, force=True,
             prior=(PRIOR_A, PRIOR_B, PRIOR_ALPHA, data.place_coords)), a.leg_steps, pairs_job, dev)
+        if not a.no_self_check:   # a short-history user: the pure-Python prior is O(h x P)
+            pu = int(np.argmin(np.abs(hist_len - 12)))
+            legs["prior"]["self_check"] = prior_self_check(
+                p_host, data, pu, pr_out[0].cpu().numpy(), pr_out[1].cpu().numpy(), K,
+                PRIOR_A, PRIOR_B, PRIOR_ALPHA)
         legs["prior"]["what"] = ("the same job ranked on the power-law-blended score (run.py:537-539): "
                                  "pr_d(dist) pair table + float64 product gather per user, score rows, "
                                  "nais_topk_blend_rows; a, b, alpha = %g, %g, %g" % (PRIOR_A, PRIOR_B, PRIOR_ALPHA))
@@ -637,15 +765,23 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             legs["region_distance"]["self_check"] = self_check(
                 p_rd, data, [1], rd_out[0].cpu().numpy(), rd_out[1].cpu().numpy(), K,
                 scorer=lambda u: nais_oracle.catalog_scores_region_distance(
-                    p_rd, data.history(int(u)), P, data.region_of, data.place_coords))
+                    p_rd, data.history(int(u)), P, data.region_of, data.place_coords),
+                oracle_name="oracle/nais_oracle.py (numpy, region_distance)")
         legs["region_distance"]["what"] = ("NAIS_region_distance_Embedding (model.py:246-297) on the same "
                                            "users / POIs: [h | region] rows, distance features from the POI "
                                            "coordinates, %s tables" % a.precision)
         del rd
+    if world == 1 and not a.no_gather_leg:
+        from poi_recommendation_models_amd import _capi
+        legs["gather_rows"] = gather_rows_leg(dev, _capi.load(), a.traffic_json)
     check = None
     if emulate == 1 and not a.no_self_check and rank == 0:   # N > 1: the merged top-k
-        ids, sc = last["out"]
-        check = self_check(p_host, data, [1, 4242 % a.num_users], ids.cpu().numpy(), sc.cpu().numpy(), K)
+        ids, sc = (t.cpu().numpy() for t in last["out"])
+        # 8 users spread over h through the torch-CPU restatement, user 1 through the numpy oracle
+        check = merge_checks(self_check(p_host, data, [1], ids, sc, K),
+                             self_check(p_host, data, spread_users(hist_len, 8), ids, sc, K,
+                                        scorer=torch_scorer(p_host, data),
+                                        oracle_name="oracle/torch_cpu.py"))
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
@@ -690,6 +826,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "fp16x3_path": legs.get("fp16x3"),
             "prior_path": legs.get("prior"),
             "region_distance_path": legs.get("region_distance"),
+            "gather_rows_path": legs.get("gather_rows"),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

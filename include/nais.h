@@ -227,11 +227,12 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *   nais_topk_keys_finish  keys -> out_ids / out_scores [num_users, k] (short lists padded with
  *                      -1 / NaN and counted into *short_count), as nais_topk_rows reports them.
  *
- * L2-blocked form of the fused route (the bench's default; DESIGN.md "gather"):
+ * L2-blocked form of the fused route (an A/B knob, off by default -- 2-3x slower than
+ * nais_pair_gather_topk so far; DESIGN.md "L2-blocked gather"):
  *   nais_pair_table_il the same pair terms as nais_pair_table in ONE interleaved, chunk-major
  *                      table: (e, es) of (row r, column c) at
  *                      table[((c-col0)/64)*chunk_stride + r*128 + ((c-col0)%64)*2];
- *                      chunk_stride >= num_items * 128 floats.
+ *                      chunk_stride >= num_items * 128 floats, and even (float2 loads).
  *   nais_pair_gather_topk_l2  nais_pair_gather_topk over such a table (num_rows = num_items):
  *                      one launch per 64-column chunk; each wave keeps up to 32 users' sums in
  *                      registers and walks the table in blocks of rows_per_block rows (a block's
@@ -270,7 +271,7 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  *                           order (1.0 for an empty history; -1.0 for history POIs) -- the bits of
  *                           nais_powerlaw_prior -- and gmax_bits[slot] = max(gmax_bits[slot], the
  *                           block's largest candidate value) as u64 bits; zero gmax_bits before the
- *                           first block.
+ *                           first block. ld must be a multiple of 4 (32-byte loads).
  *   nais_topk_blend_rows    top-k of f32((1 - alpha) * score) + alpha * g / gmax (float64; history
  *                           POIs, score < 0, excluded) per row, (score desc, id asc), as
  *                           nais_score_topk ranks with a prior; out_scores = the blended score as f32.

@@ -131,7 +131,7 @@ PAIR_MEMORY_FRACTION = 0.6      # of the device's free memory, for the tables + 
 
 
 def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlon_mat=None,
-               ordered=True, stream=None, prior=None, strategy=None):
+               ordered=True, stream=None, prior=None, strategy=None, _on_caller_stream=False):
     """Top-k (ids int64 [len(users), k], scores f32) of every listed user over its complement
     candidates, ordered (score desc, POI id asc). Raises like torch.topk when a user has fewer
     than k candidates (validation.py:26).
@@ -147,7 +147,9 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
 
     `stream` (a raw hipStream_t handle): the whole call -- its allocations, uploads, kernels and
     the final reorder -- runs on that stream, which first waits for the caller's current stream;
-    the current stream then waits for it before the results are returned."""
+    the current stream then waits for it before the results are returned. The pairs route then
+    stays on that stream alone (no CU-masked side streams), so work the caller confined to a
+    CU-masked stream stays on those CUs."""
     dev = model._check_device()
     if stream is not None:
         ext = torch.cuda.ExternalStream(stream, device=dev)
@@ -155,7 +157,7 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
         ext.wait_stream(cur)
         with torch.cuda.stream(ext):
             out = score_topk(model, train_matrix, users, k, region_of, coords, latlon_mat, ordered,
-                             None, prior, strategy)
+                             None, prior, strategy, _on_caller_stream=True)
         cur.wait_stream(ext)
         for t in out:
             t.record_stream(cur)
@@ -169,7 +171,8 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
         strategy = "pairs"
     if strategy != "direct":
         got = _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat,
-                                stream, force=strategy == "pairs", prior=prior)
+                                stream, force=strategy == "pairs", prior=prior,
+                                no_side_streams=_on_caller_stream)
         if got is not None:
             return got
     csr = device_csr(train_matrix, dev)
@@ -252,7 +255,7 @@ PAIR_TABLE_GATHER_FRAC = 0.0
 # wave keeps up to 32 users' sums of a 64-column chunk in registers while all waves walk the table
 # in blocks of PAIR_L2_ROWS rows (~1.5 MB), so the rows shared by ~50 users come from the XCD's L2
 # rather than the Infinity Cache. Same sums in the same order as nais_pair_gather_topk.
-PAIR_L2_GATHER = os.environ.get("NAIS_PAIR_L2", "0") == "1"   # A/B: slower so far
+PAIR_L2_GATHER = os.environ.get("NAIS_PAIR_L2", "0") == "1"   # A/B knob, off: 2-3x slower
 PAIR_L2_ROWS = int(os.environ.get("NAIS_PAIR_L2_ROWS", "3072"))
 PAIR_L2_WAVES_PER_CU = int(os.environ.get("NAIS_PAIR_L2_WAVES_PER_CU", "20"))
 _masked: dict = {}
@@ -330,7 +333,7 @@ def _masked_streams(dev, table_cus):
 
 
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
-                      rows_only=False, cols=None, events=None, prior=None):
+                      rows_only=False, cols=None, events=None, prior=None, no_side_streams=False):
     """Pairs strategy. `cols` = (c0, c1): score only POIs [c0, c1) (top-k ids are global POI ids;
     a column shard of sharding.distributed_topk_pairs). `events`: optional list that receives
     (kind, start, end) HIP events around every table / gather / top-k launch. `prior` = (a, b,
@@ -465,7 +468,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, G.data_ptr(), NC, c0_all,
                         gmax.data_ptr(), stream_), "nais_pair_prior_gather")
         if J > 0:
-            W = min(PAIR_BLOCK_COLS, (budget // 4) // (8 * J))
+            # two f32 tables (+ the f64 pr_d table with a prior) per buffer, <= budget / 4 each
+            W = min(PAIR_BLOCK_COLS, (budget // 4) // ((16 if prior is not None else 8) * J))
             W = int(min(NC, max(256, W // 256 * 256)))
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -473,7 +477,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                          else PAIR_TABLE_CUS)
             if events is not None:
                 events.append(("table_cus", None, None, table_cus))
-            overlap = 0 < table_cus < ncu and len(blocks) > 1 and stream is None
+            overlap = (0 < table_cus < ncu and len(blocks) > 1 and stream is None
+                       and not no_side_streams)
             gather_waves = (ncu - table_cus if overlap else ncu) * PAIR_L2_WAVES_PER_CU
             shape = ((W + 63) // 64, J, 128) if l2 else (2, J, W)
             tabs = [torch.empty(*shape, dtype=torch.float32, device=dev)

@@ -387,7 +387,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
 
 
 // ---------------------------------------------------------------------------------------------
-// L2-blocked fused gather + running top-k (the default of the fused route):
+// L2-blocked fused gather + running top-k (an A/B knob, off by default: 2-3x slower):
 // one launch per 64-column chunk of an interleaved chunk-major table (nais_pair_table_il: the
 // pair (row r, column x) at table[(x / 64) * cs + r * 128 + (x % 64) * 2] = (e, es), 512 B per
 // row and chunk). A wave owns up to UPW users (slots gw, gw + nwaves, ...: an even mix of the
@@ -793,6 +793,7 @@ int32_t nais_pair_gather_topk_l2(const float* table, int64_t chunk_stride, int64
   if (!table || !rowmap || !indptr || !indices || !users || !keys || !kcount)
     return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
   if (chunk_stride < num_rows * 128) return nais_internal_fail(NAIS_E_INVALID, "chunk_stride < num_rows * 128");
+  if (chunk_stride % 2 != 0) return nais_internal_fail(NAIS_E_INVALID, "chunk_stride must be even (float2 loads)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // users per wave: enough waves to be resident together (max_waves), at most L2_UPW per wave
   // (more users than max_waves * L2_UPW: the later waves start as the first ones retire, a few
@@ -846,6 +847,7 @@ int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowm
   if (num_users == 0 || cols == 0) return NAIS_OK;
   if (!pr || !rowmap || !indptr || !indices || !users || !g || !gmax_bits)
     return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  if (ld % 4 != 0) return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4 (32-byte loads)");
   const int64_t stripes = (cols + STRIPE - 1) / STRIPE;
   if (stripes > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "cols > 65535 * 256");
   hipLaunchKernelGGL(prior_pair_gather_kernel,

@@ -6,13 +6,17 @@ device with the fused NAIS kernel + radix-select top-k (`catalog.score_topk`), b
 (precision_v, recall_v, hit_v, precision_t, recall_t, hit_t) from `eval_metrics.evaluate_mp`.
 The model must be one of this package's NAIS modules, on a ROCm device.
 
-Multi-GPU: when a torch.distributed process group with more than one rank is initialised (one
-process per GPU, as torchrun starts them), every function here evaluates cooperatively across the
-ranks (sharding.distributed_topk: column-sharded pairs route or LPT user sharding) and returns the
-same 6-tuple on every rank, so run.py's call sites (run.py:112-116, 178-182, 259-263) stay as they
-are. Every rank must make the call.
+Multi-GPU is opt-in: pass `distributed=True` (or set NAIS_DISTRIBUTED_EVAL=1 for run.py's
+unchanged call sites, run.py:112-116, 178-182, 259-263) inside a torch.distributed process group
+of more than one rank (one process per GPU, as torchrun starts them). Every function then
+evaluates cooperatively across the ranks (sharding.distributed_topk: column-sharded pairs route or
+LPT user sharding) and returns the same 6-tuple on every rank; every rank must make the call. The
+default is the single-process path even inside a process group, so a DDP script that validates on
+rank 0 only does not block in a collective.
 """
 from __future__ import annotations
+
+import os
 
 from . import eval_metrics
 from .catalog import score_topk
@@ -28,22 +32,42 @@ def _distributed_world():
     return dist.get_world_size()
 
 
-def _recommend_ids(model, args, num_users, train_matrix, **kw):
+def _want_distributed(distributed):
+    """distributed=None reads NAIS_DISTRIBUTED_EVAL; True requires a group of > 1 rank."""
+    if distributed is None:
+        distributed = os.environ.get("NAIS_DISTRIBUTED_EVAL", "0") == "1"
+    if not distributed:
+        return False
+    if _distributed_world() <= 1:
+        raise RuntimeError("distributed evaluation needs an initialised process group of > 1 rank")
+    return True
+
+
+def _recommend_ids(model, args, num_users, train_matrix, distributed=None, **kw):
     model.eval()                                               # validation.py:8
-    if _distributed_world() > 1:
+    dist_eval = _want_distributed(distributed)
+    if dist_eval:
         from .sharding import distributed_topk
         ids, _ = distributed_topk(model, train_matrix, num_users, args.topk, **kw)
     else:
         ids, _ = score_topk(model, train_matrix, range(num_users), args.topk, **kw)
-    nan = int(model._last_nan.item())
+    nan_t = model._last_nan
+    if dist_eval:
+        # each rank counted the NaN scores of its own share: one count for the whole job,
+        # printed once (model.py:53-54 prints per forward call in one process)
+        import torch.distributed as dist
+        nan_t = nan_t.clone()
+        dist.all_reduce(nan_t)
+    nan = int(nan_t.item())
     if nan > 0 and type(model).__name__ == "NAIS_basic" and model.report_nan:
-        print(nan)                                             # model.py:53-54
+        if not dist_eval or dist.get_rank() == 0:
+            print(nan)                                         # model.py:53-54
     return ids.cpu().numpy()
 
 
-def recommend(model, args, num_users, train_matrix, **kw):
+def recommend(model, args, num_users, train_matrix, distributed=None, **kw):
     """recommended_list of validation.py:9-27: per user, args.topk POI ids, best first."""
-    return _recommend_ids(model, args, num_users, train_matrix, **kw).tolist()
+    return _recommend_ids(model, args, num_users, train_matrix, distributed, **kw).tolist()
 
 
 def _metrics(test_positive, val_positive, recommended_list, k_list):
@@ -52,22 +76,24 @@ def _metrics(test_positive, val_positive, recommended_list, k_list):
     return precision_v, recall_v, hit_v, precision_t, recall_t, hit_t
 
 
-def NAIS_validation(model, args, num_users, test_positive, val_positive, train_matrix, k_list):
+def NAIS_validation(model, args, num_users, test_positive, val_positive, train_matrix, k_list,
+                    distributed=None):
     """validation.py:7-31 (NAIS_basic)."""
-    rec = _recommend_ids(model, args, num_users, train_matrix)
+    rec = _recommend_ids(model, args, num_users, train_matrix, distributed)
     return _metrics(test_positive, val_positive, rec, k_list)
 
 
 def NAIS_region_validation(model, args, num_users, test_positive, val_positive, train_matrix,
-                           businessRegionEmbedList, k_list):
+                           businessRegionEmbedList, k_list, distributed=None):
     """validation.py:34-59 (NAIS_regionEmbedding)."""
-    rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList)
+    rec = _recommend_ids(model, args, num_users, train_matrix, distributed,
+                         region_of=businessRegionEmbedList)
     return _metrics(test_positive, val_positive, rec, k_list)
 
 
 def NAIS_region_distance_validation(model, args, num_users, test_positive, val_positive,
                                     train_matrix, businessRegionEmbedList, latlon_mat, k_list,
-                                    poi_coords=None):
+                                    poi_coords=None, distributed=None):
     """validation.py:62-131 (NAIS_region_distance_Embedding).
 
     The reference reads (|dlat|, |dlng|) from a P x P x 2 float64 `latlon_mat` (run.py:47-54,214).
@@ -78,16 +104,16 @@ def NAIS_region_distance_validation(model, args, num_users, test_positive, val_p
     """
     _ = args.powerlaw_weight
     if poi_coords is not None:
-        rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
-                        coords=poi_coords)
+        rec = _recommend_ids(model, args, num_users, train_matrix, distributed,
+                             region_of=businessRegionEmbedList, coords=poi_coords)
     else:
-        rec = _recommend_ids(model, args, num_users, train_matrix, region_of=businessRegionEmbedList,
-                        latlon_mat=latlon_mat)
+        rec = _recommend_ids(model, args, num_users, train_matrix, distributed,
+                             region_of=businessRegionEmbedList, latlon_mat=latlon_mat)
     return _metrics(test_positive, val_positive, rec, k_list)
 
 
 def new4_validation(model, args, num_users, test_positive, val_positive, train_matrix,
-                    businessRegionEmbedList, k_list, nearPOI):
+                    businessRegionEmbedList, k_list, nearPOI, distributed=None):
     """validation.py:254-280 (New4): the context tables are built once (the reference rebuilds
     them in every 1,024-candidate chunk), then every user's catalog is scored with the basic
     kernels. Differs from the reference only where it breaks: with <= 1,024 candidates the
@@ -95,5 +121,5 @@ def new4_validation(model, args, num_users, test_positive, val_positive, train_m
     users are scored normally."""
     model.eval()
     model.extended_tables(nearPOI)
-    rec = _recommend_ids(model, args, num_users, train_matrix)
+    rec = _recommend_ids(model, args, num_users, train_matrix, distributed)
     return _metrics(test_positive, val_positive, rec, k_list)

@@ -3,8 +3,8 @@
 * config 4 -- the benchmarked path itself: the bench's whole job (50k users x 100k POIs,
   d = H = 64, h ~ U{1..200}, the bench's seeds) through catalog._score_topk_pairs with the bench's
   default knobs (fp16x6 tables, CU-masked overlap, 512-column blocks, fused running top-k,
-  longest-first order). Every user's top-50 against the per-user ("direct") kernels, 4 users
-  against the numpy oracle.
+  longest-first order). Every user's top-50 against the per-user ("direct") kernels; 32 users
+  spread over h against the CPU restatements (torch_cpu + the numpy oracle for two).
 * config 2 -- P = 50k, d = H = 64, h <= 100: a 600-user slice through both routes vs each other
   and vs the oracle.
 * config 5 -- P = 1M, d = H = 128, h <= 200: 8 users through the direct route (full rows + top-50)
@@ -50,24 +50,35 @@ def _stats(tag, before):
           f"{d['inexact_runs']} of them not exact fp32 ties")
 
 
-def test_config4_bench_job_pairs_vs_direct_and_oracle():
+@pytest.fixture(scope="module")
+def config4_job():
+    """The bench's whole config-4 job through the pairs route with the bench's knobs, once per
+    module: (data, params, ids, scores)."""
     from poi_recommendation_models_amd import catalog
-    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs, score_topk
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
-    before = dict(TIE_STATS)
     U, P, D, H, K = 50_000, 100_000, 64, 64, 50
     data = make_checkins(U, P, 200, seed=2024)                   # bench.py's workload
     p = init_nais_params(P, D, H, seed=7, emb_std=0.3, bias_std=0.1)
     m = _model(p, P, D, H)
     assert m.precision == "fp16x6"
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
-    users = np.arange(U)
     ev = []
-    ids, sc = _score_topk_pairs(m, csr, users, K, None, None, None, None, force=True, events=ev)
+    ids, sc = _score_topk_pairs(m, csr, np.arange(U), K, None, None, None, None, force=True, events=ev)
     settings = {k: n for k, a, b, n in ev if a is None}
     assert settings["table_cus"] not in (0, torch.cuda.get_device_properties(DEV).multi_processor_count)
     assert catalog.PAIR_FUSED_TOPK and catalog.PAIR_LPT_ORDER and catalog.PAIR_BLOCK_COLS == 512
-    ids_p, sc_p = ids.cpu().numpy(), sc.cpu().numpy()
+    return data, p, m, csr, ids.cpu().numpy(), sc.cpu().numpy()
+
+
+def test_config4_bench_job_pairs_vs_direct(config4_job):
+    """Every one of the 50k users' top-50 lists: pairs route (the bench) against the per-user
+    kernels (a self-comparison of the build's two routes; the oracle check is the next test)."""
+    from poi_recommendation_models_amd.catalog import score_topk
+    before = dict(TIE_STATS)
+    data, p, m, csr, ids_p, sc_p = config4_job
+    U, K = data.num_users, 50
+    users = np.arange(U)
     ids_d, sc_d = score_topk(m, csr, users, K, strategy="direct")
     ids_d, sc_d = ids_d.cpu().numpy(), sc_d.cpu().numpy()
     hist_ok = all(not np.isin(ids_p[u], data.history(u)).any() for u in range(0, U, 97))
@@ -77,18 +88,53 @@ def test_config4_bench_job_pairs_vs_direct_and_oracle():
     print(f"config 4: {U} users, {nd} lists differ from the direct route in some position "
           f"(resolved by the tie rule, {runs} tie runs), max |score| diff at equal positions "
           f"{np.max(np.abs(sc_p - sc_d)):.3g}")
-    # 4 users against the numpy oracle: the shortest, the longest and two others
+    _stats("config 4 pairs vs direct", before)
+
+
+def _config4_oracle_users(h, n=32):
+    """n users spread over the history lengths: the shortest, the longest and the quantiles
+    in between (distinct users)."""
+    order = np.argsort(h, kind="stable")
+    pos = np.unique(np.round(np.linspace(0, len(order) - 1, n)).astype(np.int64))
+    return [int(u) for u in order[pos]]
+
+
+def test_config4_bench_job_vs_reference_restatement(config4_job):
+    """32 users of the bench job, spread over h (shortest, longest, quantiles),
+    against the CPU restatements: each user's full catalog through oracle/torch_cpu.py (the
+    reference's loop in torch CPU ops, pinned to the reference's own outputs by
+    tests/test_torch_cpu_baseline.py), tie-aware top-50 and scores; for 2 of them (the shortest
+    and the median history) also the numpy oracle (oracle/nais_oracle.py)."""
+    from oracle import torch_cpu
+    before = dict(TIE_STATS)
+    data, p, m, csr, ids_p, sc_p = config4_job
+    P, K = data.num_pois, 50
     h = data.hist_len()
-    for u in (int(np.argmin(h)), int(np.argmax(h)), 1, 4242):
-        cand, ref = nais_oracle.catalog_scores_basic(p, data.history(u), P, chunk=4096)
+    users = _config4_oracle_users(h)
+    assert len(users) == 32 and h[users[0]] == h.min() and h[users[-1]] == h.max()
+    tm = torch_cpu.TorchNAIS(p)
+    worst = 0.0
+    for i, u in enumerate(users):
+        hist = data.history(u)
+        rows, cand = torch_cpu.candidates(hist, P)
+        with torch.no_grad():
+            ref = torch.cat([tm(rows[c:c + 1024], cand[c:c + 1024])
+                             for c in range(0, len(cand), 1024)]).numpy()
+        cand = cand.numpy()
+        if i in (0, len(users) // 2):     # the shortest and the median also through numpy
+            ocand, oref = nais_oracle.catalog_scores_basic(p, hist, P, chunk=4096)
+            np.testing.assert_array_equal(ocand, cand)
+            assert np.max(np.abs(oref - ref)) <= 1e-6
         rid, rsc = nais_oracle.topk_ids(cand, ref, K)
         lookup = dict(zip(cand.tolist(), ref.tolist()))
         assert_topk_equivalent(rid, rsc, ids_p[u], sc_p[u], tie_ulps=TIE_ULPS, lookup=lookup)
         got = np.array([lookup[int(c)] for c in ids_p[u]])
-        assert np.max(np.abs(got - sc_p[u])) <= SCORE_ATOL
-        print(f"  user {u} (h={h[u]}): max |score - oracle| over its top-50 "
-              f"{np.max(np.abs(got - sc_p[u])):.3g}")
-    _stats("config 4", before)
+        d = float(np.max(np.abs(got - sc_p[u])))
+        assert d <= SCORE_ATOL
+        worst = max(worst, d)
+    print(f"config 4: {len(users)} users (h = {h[users[0]]} .. {h[users[-1]]}) vs the restatement: "
+          f"max |score - reference restatement| over their top-50 {worst:.3g}")
+    _stats("config 4 vs restatement", before)
 
 
 def test_config2_slice_both_routes():

@@ -79,10 +79,12 @@ def _positives(data, seed):
 
 
 def _worker_validation(rank, world, port, kind, out):
-    """validation.NAIS_validation itself, called by every rank inside the process group."""
+    """validation.NAIS_validation itself, called by every rank inside the process group with the
+    distributed route switched on (NAIS_DISTRIBUTED_EVAL=1: run.py's call sites unchanged)."""
     import torch.distributed as dist
     from poi_recommendation_models_amd import validation as V
     torch.cuda.set_device(0)
+    os.environ["NAIS_DISTRIBUTED_EVAL"] = "1"
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     data, p = _data(kind)
     m = _model(p, data.num_pois)
@@ -98,7 +100,7 @@ def _worker_validation(rank, world, port, kind, out):
 
 @pytest.mark.parametrize("kind", ["shared", "sparse"])
 def test_validation_autoroute_two_ranks_equal_single(kind):
-    """run.py:112-116 unchanged under torchrun: NAIS_validation in a 2-rank group (column-sharded
+    """run.py:112-116 unchanged under torchrun + NAIS_DISTRIBUTED_EVAL=1: NAIS_validation in a 2-rank group (column-sharded
     pairs or user-sharded route) returns the single-process 6-tuple on every rank."""
     import torch.multiprocessing as mp
     from poi_recommendation_models_amd import validation as V

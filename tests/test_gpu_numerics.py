@@ -161,3 +161,74 @@ def test_score_topk_on_caller_stream(strategy):
         ids, sc = score_topk(m, csr, range(U), 50, strategy=strategy, stream=s.cuda_stream)
         ids2 = ids + 0                      # consumed on the current stream right away
         assert torch.equal(ids2, ref_i) and torch.equal(sc, ref_s)
+
+
+def _heterogeneous(p, D, H):
+    """Rows of very different magnitude side by side (the fp16x6 kernels scale the candidate rows
+    of a wave, and the item rows of a 32-item chunk, by one power of two): every 4th row at the
+    reference's N(0, 0.01) init (model.py:32-33) among N(0, 0.3) rows, every 8th row 2^-12 below
+    its neighbours, every 16th row all zero."""
+    q = {k: v.copy() for k, v in p.items()}
+    for name in ("embed_history.weight", "embed_target.weight"):
+        w = q[name]
+        r = np.arange(w.shape[0])
+        w[r % 4 == 1] *= np.float32(0.01 / 0.3)
+        w[r % 8 == 2] *= np.float32(2.0 ** -12)
+        w[r % 16 == 3] = 0.0
+    return q
+
+
+@pytest.mark.parametrize("D,H", [(64, 64), (128, 128)])
+def test_fp16x6_is_fp32_faithful_heterogeneous_rows(D, H):
+    """pair-table entries with small / zero rows beside large ones in the same
+    wave and chunk: fp16x6's error stays within 2x of the exact-fp32 kernel's (max and mean)."""
+    from poi_recommendation_models_amd.synthetic import init_nais_params
+    P = 3000
+    p = _heterogeneous(init_nais_params(P, D, H, seed=5 + D, emb_std=0.3, bias_std=0.1), D, H)
+    items = np.sort(np.random.default_rng(2).choice(P, 96, replace=False))
+    c0, c1 = 512, 2560
+    e64, es64, es_scale = _tables64(p, items, c0, c1)
+    err = {}
+    for prec in ("fp32", "fp16x6"):
+        e, es = _tables_gpu(_model(p, P, D, H, prec), items, c0, c1)
+        re = np.abs(e - e64) / np.maximum(np.abs(e64), 1e-30)
+        rs = np.abs(es - es64) / np.maximum(es_scale, 1e-30)
+        rs = np.where(es_scale > 0, rs, np.abs(es - es64))          # zero rows: es must be 0
+        err[prec] = (re.max(), re.mean(), rs.max(), rs.mean())
+        print(f"D={D} H={H} {prec:7s}: e rel err max {re.max():.3g} mean {re.mean():.3g}; "
+              f"es err max {rs.max():.3g} mean {rs.mean():.3g}")
+    for i in range(4):
+        assert err["fp16x6"][i] <= 2.0 * err["fp32"][i] + 1e-12, (i, err)
+
+
+def _scores64(p, hist, P, beta=0.5):
+    """float64 full-catalog scores of one user (model.py:57-89, validation.py:11-22); history
+    POIs -> -1."""
+    e, es, _ = _tables64(p, np.asarray(hist), 0, P)
+    S, N = e.sum(0), es.sum(0)
+    logit = np.where(len(hist) > 0, N / np.power(S, beta), 0.0)
+    sc = 1.0 / (1.0 + np.exp(-logit))
+    sc[np.asarray(hist, dtype=np.int64)] = -1.0
+    return sc
+
+
+@pytest.mark.parametrize("D,H", [(64, 64), (128, 128)])
+def test_fp16x6_direct_scores_faithful_heterogeneous_rows(D, H):
+    """The per-user (direct) catalog kernel on the same heterogeneous rows: fp16x6 scores within
+    2x of the exact-fp32 kernel's error against float64 (max and mean over the candidates)."""
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P, U = 2500, 4
+    data = make_checkins(U, P, 70, seed=9)
+    p = _heterogeneous(init_nais_params(P, D, H, seed=11 + D, emb_std=0.3, bias_std=0.1), D, H)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    ref = np.stack([_scores64(p, data.history(u), P) for u in range(U)])
+    cand = ref >= 0
+    err = {}
+    for prec in ("fp32", "fp16x6"):
+        got = score_catalog(_model(p, P, D, H, prec), csr, range(U), strategy="direct").cpu().numpy()
+        d = np.abs(got.astype(np.float64) - ref)[cand]
+        err[prec] = (d.max(), d.mean())
+        print(f"D={D} H={H} {prec}: |dscore| max {d.max():.3g} mean {d.mean():.3g}")
+    assert err["fp16x6"][0] <= 2.0 * err["fp32"][0] + 1e-12, err
+    assert err["fp16x6"][1] <= 2.0 * err["fp32"][1] + 1e-12, err

@@ -158,6 +158,14 @@ def test_catalog_golden(variant, tag, precision, strategy):
     print(f"{variant}/{tag}/{precision}: max |score - reference| = {worst:.3g}")
 
 
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
+@pytest.mark.parametrize("variant", ["basic", "region_distance"])
+def test_catalog_golden_fp16x3_pairsplit(variant, strategy):
+    """fp16x3_pairsplit (the per-pair split kernel at fp16x3 arithmetic) is still an
+    exported precision; keep one golden case per route for it."""
+    test_catalog_golden(variant, "trained", "fp16x3_pairsplit", strategy)
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_validation_dropin_metrics(precision):
     """validation.NAIS_validation returns the reference's 6-tuple on the golden dataset."""

@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 
 from _helpers import load_golden, params_from, positives_from
@@ -118,9 +119,11 @@ def test_sharded_table_allgather_world2():
     np.testing.assert_array_equal(res[0][3], res[1][3])   # MLP broadcast from rank 0
 
 
-def _worker_validation(rank, world, port, q):
-    """validation.NAIS_validation inside a world-2 gloo group routes to sharding.distributed_topk
-    (run.py:112-116 unchanged). The device scorer is replaced by the oracle here (CPU test); the
+def _worker_validation(rank, world, port, q, mode="env"):
+    """validation.NAIS_validation inside a world-2 gloo group. mode "env" (NAIS_DISTRIBUTED_EVAL=1,
+    run.py:112-116 unchanged) and "kw" (distributed=True) route to sharding.distributed_topk on
+    every rank; "default" stays single-process, and only rank 0 calls (the DDP pattern that must
+    not block in a collective). The device scorers are replaced by the oracle here (CPU test); the
     user sharding, the all-gather of the [users, k] blocks and the metrics are the product code."""
     import scipy.sparse as sp
     import torch.distributed as dist
@@ -149,8 +152,19 @@ def _worker_validation(rank, world, port, q):
                            num_users, group=group)
     sharding.distributed_topk = oracle_distributed_topk
 
+    def oracle_score_topk(model, train_matrix, users, k, **kw):
+        calls.append(("single", len(users)))
+        ids = []
+        for u in users:
+            hist = train_matrix.indices[train_matrix.indptr[u]:train_matrix.indptr[u + 1]]
+            ids.append(nais_oracle.topk_ids(*nais_oracle.catalog_scores_basic(p, hist, P), k)[0])
+        return torch.as_tensor(np.array(ids).reshape(-1, k)), None
+    V.score_topk = oracle_score_topk
+    if mode == "env":
+        os.environ["NAIS_DISTRIBUTED_EVAL"] = "1"
+
     class Model:                      # what _recommend_ids touches on the module
-        report_nan = False
+        report_nan = True
         _last_nan = torch.zeros((), dtype=torch.int32)
 
         def eval(self):
@@ -159,25 +173,34 @@ def _worker_validation(rank, world, port, q):
     class Args:
         topk = 50
     X = sp.csr_matrix((np.ones(len(z["indices"])), z["indices"], z["indptr"]), shape=(U, P))
-    got = V.NAIS_validation(Model(), Args(), U, positives_from(z, "test"), positives_from(z, "val"),
-                            X, [5, 10, 15, 20, 25, 30])
-    q.put((rank, calls, np.array(got)))
+    got = None
+    if mode != "default" or rank == 0:
+        got = np.array(V.NAIS_validation(Model(), Args(), U, positives_from(z, "test"),
+                                         positives_from(z, "val"), X, [5, 10, 15, 20, 25, 30],
+                                         **({"distributed": True} if mode == "kw" else {})))
+    q.put((rank, calls, got))
+    dist.barrier()
     dist.destroy_process_group()
 
 
-def test_validation_autoroutes_world2():
+@pytest.mark.parametrize("mode", ["env", "kw", "default"])
+def test_validation_distributed_opt_in_world2(mode):
     ctx = mp.get_context("fork")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_validation, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker_validation, args=(r, 2, port, q, mode)) for r in range(2)]
     for pr in procs:
         pr.start()
-    res = [q.get(timeout=120) for _ in range(2)]
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
     z = load_golden("catalog_basic.npz")
     U = int(z["num_users"])
+    if mode == "default":                                   # rank 0 alone, single-process path
+        assert res[0][1] == [("single", U)] and res[1][1] == [] and res[1][2] is None
+        np.testing.assert_allclose(res[0][2], z["trained/metrics"], atol=2.0 / U)
+        return
     for rank, calls, got in res:
         assert calls == [U], calls                          # went through the distributed path
         np.testing.assert_allclose(got, z["trained/metrics"], atol=2.0 / U)
