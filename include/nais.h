@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 6
+#define NAIS_ABI_VERSION 7
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -275,6 +275,13 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  *   nais_topk_blend_rows    top-k of f32((1 - alpha) * score) + alpha * g / gmax (float64; history
  *                           POIs, score < 0, excluded) per row, (score desc, id asc), as
  *                           nais_score_topk ranks with a prior; out_scores = the blended score as f32.
+ *   nais_topk_blend_rows_f64  the same, and (out_blend != NULL) the f64 blended score of every
+ *                           returned candidate (NaN for padding) -- the key a column-sharded job
+ *                           merges on.
+ *   nais_topk_merge_f64     merge of per-column-block lists: row r's m candidates
+ *                           (keys[r*m + i] f64, ids[r*m + i] global POI ids, id < 0 = padding) ->
+ *                           the k best by (key desc, id asc), NaN first, as out_ids / out_scores
+ *                           (f32) / out_keys (f64, optional). m <= 2048, k <= m.
  */
 int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int64_t* items,
                               int64_t num_items, int64_t col0, int64_t cols, double a, double b,
@@ -287,6 +294,13 @@ int32_t nais_topk_blend_rows(const float* scores, int64_t score_ld, const double
                              const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
                              double alpha, int32_t* out_ids, float* out_scores, int32_t* short_count,
                              void* stream);
+int32_t nais_topk_blend_rows_f64(const float* scores, int64_t score_ld, const double* g, int64_t g_ld,
+                                 const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
+                                 double alpha, int32_t* out_ids, float* out_scores, double* out_blend,
+                                 int32_t* short_count, void* stream);
+int32_t nais_topk_merge_f64(const double* keys, const int64_t* ids, int32_t num_rows, int32_t m,
+                            int32_t k, int64_t* out_ids, float* out_scores, double* out_keys,
+                            void* stream);
 int32_t nais_pair_table_il(const nais_params_t* params, const int64_t* items, int64_t num_items,
                            int64_t col0, int64_t cols, const int64_t* region_of,
                            const double* coords, const double* latlon_mat, float* table,

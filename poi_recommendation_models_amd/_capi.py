@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE, VARIANT_DISTANCE = 0, 1, 2, 3
@@ -30,7 +30,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
            "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
            "nais_pair_table_il", "nais_pair_gather_topk_l2", "nais_pair_prior_table",
-           "nais_pair_prior_gather", "nais_topk_blend_rows")
+           "nais_pair_prior_gather", "nais_topk_blend_rows", "nais_topk_blend_rows_f64",
+           "nais_topk_merge_f64")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -208,6 +209,10 @@ def load(path: str | None = None):
     lib.nais_pair_prior_gather.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, vp, i64, i64, vp, vp]
     lib.nais_topk_blend_rows.restype = i32
     lib.nais_topk_blend_rows.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp]
+    lib.nais_topk_blend_rows_f64.restype = i32
+    lib.nais_topk_blend_rows_f64.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp, vp]
+    lib.nais_topk_merge_f64.restype = i32
+    lib.nais_topk_merge_f64.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp]
     lib.nais_topk_keys_finish.restype = i32
     lib.nais_topk_keys_finish.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32

@@ -333,12 +333,20 @@ def _masked_streams(dev, table_cus):
 
 
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
-                      rows_only=False, cols=None, events=None, prior=None, no_side_streams=False):
+                      rows_only=False, cols=None, events=None, prior=None, no_side_streams=False,
+                      group=None, return_keys=False):
     """Pairs strategy. `cols` = (c0, c1): score only POIs [c0, c1) (top-k ids are global POI ids;
     a column shard of sharding.distributed_topk_pairs). `events`: optional list that receives
     (kind, start, end) HIP events around every table / gather / top-k launch. `prior` = (a, b,
     alpha, poi_coords): rank on the power-law-blended score (score_topk); score rows + float64 G
-    rows per pass, then nais_topk_blend_rows (the direct route's blend, same G bits)."""
+    rows per pass, then nais_topk_blend_rows (the direct route's blend, same G bits).
+
+    Column shards with a prior (`cols` and `group`, a torch.distributed group whose ranks own
+    the other columns): every rank makes the same number of user passes (MIN all-reduce of the
+    users one pass can hold), and each user's max G over ITS columns is MAX all-reduced before the
+    blend, so every rank normalises by the whole catalog's max (run.py:55-59) -- one [users]
+    int64 collective per pass. `return_keys`: also return the f64 blended score of each returned
+    candidate (the merge key of sharding.distributed_topk_pairs)."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model._item_tables()[0].shape[0]
@@ -394,8 +402,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     free = torch.cuda.mem_get_info(dev)[0]
     budget = int(free * PAIR_MEMORY_FRACTION)
     from .model import _NAISDevice
-    if prior is not None and (cols is not None or rows_only or model._pairs_only):
-        raise NotImplementedError("the pairs route blends the prior over whole rows of NAIS models only")
+    if prior is not None and (rows_only or model._pairs_only):
+        raise NotImplementedError("the pairs route blends the prior over the rows of NAIS models only")
+    if prior is not None and cols is not None and (c0_all, c1_all) != (0, P) and group is None:
+        raise ValueError("a prior over a column shard needs the process group of the other shards "
+                         "(the normaliser max G runs over the whole catalog)")
     fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256 and prior is None
              and type(model)._pair_fixup is _NAISDevice._pair_fixup)
     if prior is not None:
@@ -421,6 +432,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     # budget (fused: no score rows)
     row_bytes = 4 * NC + (8 * NC if prior is not None else 0)
     per_pass = n if (rows_only or fused) else max(1, min(n, (budget // 2) // row_bytes))
+    if prior is not None and group is not None:     # the same passes (and collectives) on every rank
+        from .sharding import agree_min
+        per_pass = agree_min(per_pass, dev, group)
+    keys_out = torch.empty(n, k, dtype=torch.float64, device=dev) if return_keys else None
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
     sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -555,10 +570,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             if J == 0:      # empty histories: G = prod over nothing = 1.0 for every candidate
                 G.fill_(1.0)
                 gmax.fill_(int(np.array(1.0).view(np.int64)))
-            timed("topk", lambda: _capi.check(lib.nais_topk_blend_rows(
+            if group is not None:   # normalise by the max over every rank's columns
+                from .sharding import allreduce_gmax
+                allreduce_gmax(gmax, group)
+            timed("topk", lambda: _capi.check(lib.nais_topk_blend_rows_f64(
                 scores.data_ptr(), NC, G.data_ptr(), NC, gmax.data_ptr(), NC, m, k, float(alpha),
-                ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(), counters[1:2].data_ptr(),
-                st), "nais_topk_blend_rows"))
+                ids_out[b0:b0 + m].data_ptr(), sc_out[b0:b0 + m].data_ptr(),
+                keys_out[b0:b0 + m].data_ptr() if return_keys else None, counters[1:2].data_ptr(),
+                st), "nais_topk_blend_rows_f64"))
             del G, gmax
         else:
             timed("topk", lambda: _capi.check(lib.nais_topk_rows(
@@ -572,6 +591,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if order is not None:           # back to the caller's user order
         inv = up_dev[n:]
         ids, sc_out = ids.index_select(0, inv), sc_out.index_select(0, inv)
+        if return_keys:
+            keys_out = keys_out.index_select(0, inv)
+    if return_keys:
+        return ids, sc_out, keys_out
     return ids, sc_out
 
 

@@ -1730,7 +1730,8 @@ __global__ void __launch_bounds__(TOPK_THREADS)
 topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const double* __restrict__ G,
                   int64_t g_ld, const unsigned long long* __restrict__ gmax, int64_t P, int k,
                   float om_alpha_f, double alpha, int32_t* __restrict__ out_ids,
-                  float* __restrict__ out_scores, int32_t* __restrict__ short_count) {
+                  float* __restrict__ out_scores, int32_t* __restrict__ short_count,
+                  double* __restrict__ out_blend) {
   __shared__ uint32_t hist[256];
   __shared__ unsigned long long bs[BLEND_CAP];
   __shared__ uint32_t bi[BLEND_CAP];
@@ -1865,15 +1866,76 @@ topk_blend_kernel(const float* __restrict__ scores, int64_t score_ld, const doub
   }
   for (int i = tid; i < k; i += TOPK_THREADS) {
     int32_t id = -1;
-    float sc = __builtin_nanf("");
+    double v = __builtin_nan("");
     if (i < kk) {
       id = (int32_t)(0xFFFFFFFFu - bi[i]);
-      sc = (float)unord_f64(bs[i]);
+      v = unord_f64(bs[i]);
     }
     out_ids[(int64_t)blockIdx.x * k + i] = id;
-    out_scores[(int64_t)blockIdx.x * k + i] = sc;
+    out_scores[(int64_t)blockIdx.x * k + i] = (float)v;
+    if (out_blend) out_blend[(int64_t)blockIdx.x * k + i] = v;   // the f64 ranking key itself
   }
   if (tid == 0 && kk < k && short_count) atomicAdd(short_count, 1);
+}
+
+// Merge of per-column-block top-k lists ranked on f64 blended scores (the column-sharded prior
+// route, sharding.distributed_topk_pairs): row r holds m candidates (keys[r*m + i] f64, ids[r*m + i]
+// global POI ids, id < 0 = padding); out = the k best by (key desc, id asc), NaN first -- the
+// order topk_blend_kernel gives one whole row. One workgroup per row, bitonic sort in LDS.
+constexpr int MERGE_THREADS = 256, MERGE_CAP = 2048;
+__global__ void __launch_bounds__(MERGE_THREADS)
+topk_merge_f64_kernel(const double* __restrict__ keys, const int64_t* __restrict__ ids, int m, int k,
+                      int64_t* __restrict__ out_ids, float* __restrict__ out_scores,
+                      double* __restrict__ out_keys) {
+  __shared__ unsigned long long sk[MERGE_CAP];
+  __shared__ long long si[MERGE_CAP];
+  const int tid = threadIdx.x;
+  const int64_t r = blockIdx.x;
+  int n2 = 1;
+  while (n2 < m) n2 <<= 1;
+  for (int i = tid; i < n2; i += MERGE_THREADS) {
+    unsigned long long key = 0ull;                 // padding: below every real key (> 0)
+    long long id = 0x7fffffffffffffffll;
+    if (i < m) {
+      const long long x = ids[r * m + i];
+      if (x >= 0) {
+        key = ord_f64(keys[r * m + i]);
+        id = x;
+      }
+    }
+    sk[i] = key;
+    si[i] = id;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2; i += MERGE_THREADS) {
+        const int partner = i ^ stride;
+        if (partner > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long x = sk[i], y = sk[partner];
+          const long long xi = si[i], yi = si[partner];
+          // "better" = larger key, then smaller id
+          const bool x_worse = (x < y) || (x == y && xi > yi);
+          const bool x_better = (x > y) || (x == y && xi < yi);
+          if (desc ? x_worse : x_better) {
+            sk[i] = y;
+            sk[partner] = x;
+            si[i] = yi;
+            si[partner] = xi;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += MERGE_THREADS) {
+    const bool ok = i < n2 && sk[i] != 0ull;
+    const double v = ok ? unord_f64(sk[i]) : __builtin_nan("");
+    out_ids[r * k + i] = ok ? (int64_t)si[i] : -1;
+    out_scores[r * k + i] = (float)v;
+    if (out_keys) out_keys[r * k + i] = v;
+  }
 }
 
 // Distance histogram for PowerLaw.fit_distance_distribution (powerLaw.py:41-55): every pair
@@ -2319,7 +2381,8 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
       if (rc) return rc;
       hipLaunchKernelGGL(topk_blend_kernel, dim3(nb), dim3(TOPK_THREADS), 0, st, scores, ld, G, ld,
                          gmax, params->num_pois, k, (float)(1.0 - prior->alpha), prior->alpha,
-                         out_ids + (int64_t)u0 * k, out_scores + (int64_t)u0 * k, short_count);
+                         out_ids + (int64_t)u0 * k, out_scores + (int64_t)u0 * k, short_count,
+                         (double*)nullptr);
       rc = check_launch("topk_blend_kernel");
       if (rc) return rc;
     }
@@ -2489,6 +2552,34 @@ int32_t nais_topk_blend_rows(const float* scores, int64_t score_ld, const double
                              const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
                              double alpha, int32_t* out_ids, float* out_scores, int32_t* short_count,
                              void* stream) {
+  return nais_topk_blend_rows_f64(scores, score_ld, g, g_ld, gmax_bits, num_pois, num_rows, k, alpha,
+                                  out_ids, out_scores, nullptr, short_count, stream);
+}
+
+int32_t nais_topk_merge_f64(const double* keys, const int64_t* ids, int32_t num_rows, int32_t m,
+                            int32_t k, int64_t* out_ids, float* out_scores, double* out_keys,
+                            void* stream) {
+  if (num_rows < 0 || m <= 0 || k <= 0 || k > m) return fail(NAIS_E_INVALID, "bad shape");
+  if (m > MERGE_CAP) return fail(NAIS_E_UNSUPPORTED, "m > 2048 candidates per row");
+  if (num_rows == 0) return NAIS_OK;
+  if (!keys || !ids || !out_ids || !out_scores) return fail(NAIS_E_INVALID, "missing pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int32_t r0 = 0; r0 < num_rows; r0 += 65535) {
+    const int nb = std::min<int32_t>(65535, num_rows - r0);
+    hipLaunchKernelGGL(topk_merge_f64_kernel, dim3(nb), dim3(MERGE_THREADS), 0, st,
+                       keys + (int64_t)r0 * m, ids + (int64_t)r0 * m, (int)m, (int)k,
+                       out_ids + (int64_t)r0 * k, out_scores + (int64_t)r0 * k,
+                       out_keys ? out_keys + (int64_t)r0 * k : nullptr);
+    const int rc = check_launch("topk_merge_f64_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_topk_blend_rows_f64(const float* scores, int64_t score_ld, const double* g, int64_t g_ld,
+                                 const uint64_t* gmax_bits, int64_t num_pois, int32_t num_rows, int32_t k,
+                                 double alpha, int32_t* out_ids, float* out_scores, double* out_blend,
+                                 int32_t* short_count, void* stream) {
   if (num_rows < 0 || num_pois <= 0 || k <= 0 || score_ld < num_pois || g_ld < num_pois)
     return fail(NAIS_E_INVALID, "bad shape");
   if (k > MAX_K) return fail(NAIS_E_UNSUPPORTED, "k > 1024");
@@ -2501,7 +2592,7 @@ int32_t nais_topk_blend_rows(const float* scores, int64_t score_ld, const double
                        score_ld, g + (int64_t)r0 * g_ld, g_ld,
                        reinterpret_cast<const unsigned long long*>(gmax_bits) + r0, num_pois, k,
                        (float)(1.0 - alpha), alpha, out_ids + (int64_t)r0 * k, out_scores + (int64_t)r0 * k,
-                       short_count);
+                       short_count, out_blend ? out_blend + (int64_t)r0 * k : nullptr);
     const int rc = check_launch("topk_blend_kernel");
     if (rc) return rc;
   }

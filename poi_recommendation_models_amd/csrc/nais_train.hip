@@ -877,6 +877,19 @@ __device__ __forceinline__ float tfull(const GArgs& a, int64_t c, int d) {
   return a.er[a.treg[c] * a.RDIM + (d - a.IDIM)];
 }
 
+// Shape of one general-kernel instantiation: compile-time D / H / extra input dims where the
+// template fixes them (the reference defaults, D = H = 128: every loop below then has a constant
+// trip count, is unrolled and its LDS operand reads are scheduled ahead of the MFMAs), the
+// runtime GArgs values otherwise (DC = 0).
+struct GS {
+  int D, H, DIN;
+};
+template <int DC, int HC, int XC>
+__device__ __forceinline__ GS make_gs(const GArgs& a) {
+  if constexpr (DC > 0) return GS{DC, HC, DC + XC};
+  else return GS{a.D, a.H, a.DIN};
+}
+
 // LDS image of the general kernels (floats). Hidden rows are padded to HB*32 (zeros), x to
 // DINP = DIN rounded up to even (K-steps of 2); pitches are odd so that every MFMA operand read
 // (lanes over rows at a fixed column, or over columns at a fixed row) is bank-conflict-free.
@@ -914,27 +927,27 @@ struct GL {
 
 // stage W1 (row-major, pitch Q, zero padded), b1, w2, the slice's full history rows and the
 // workgroup's full target rows (+ the distance features of every (row, item) pair)
-__device__ void gm_stage(const GArgs& a, const GL& g, float* L, int tid, int64_t c0, int64_t j0,
-                         int nj) {
+__device__ __forceinline__ void gm_stage(const GArgs& a, const GS& s, const GL& g, float* L, int tid,
+                                         int64_t c0, int64_t j0, int nj) {
   constexpr int NT = GW * 64;
   for (int f = tid; f < g.HP32 * g.Q; f += NT) {
     const int i = f / g.Q, k = f % g.Q;
-    L[g.o_w1 + f] = (i < a.H && k < a.DIN) ? a.w1[int64_t(i) * a.DIN + k] : 0.f;
+    L[g.o_w1 + f] = (i < s.H && k < s.DIN) ? a.w1[int64_t(i) * s.DIN + k] : 0.f;
   }
   for (int i = tid; i < g.HP32; i += NT) {
-    L[g.o_b1 + i] = i < a.H ? a.b1[i] : 0.f;
-    L[g.o_w2 + i] = i < a.H ? a.w2[i] : 0.f;
+    L[g.o_b1 + i] = i < s.H ? a.b1[i] : 0.f;
+    L[g.o_w2 + i] = i < s.H ? a.w2[i] : 0.f;
   }
   for (int f = tid; f < 32 * g.HD; f += NT) {
     const int n = f / g.HD, d = f % g.HD;
-    L[g.o_hs + f] = (n < nj && d < a.D) ? hfull(a, j0 + n, d) : 0.f;
+    L[g.o_hs + f] = (n < nj && d < s.D) ? hfull(a, j0 + n, d) : 0.f;
   }
-  for (int f = tid; f < GW * a.D; f += NT) {
-    const int w = f / a.D, d = f % a.D;
+  for (int f = tid; f < GW * s.D; f += NT) {
+    const int w = f / s.D, d = f % s.D;
     const int64_t c = c0 + w;
     L[g.o_ts + f] = c < a.b ? tfull(a, c, d) : 0.f;
   }
-  if (a.DIN > a.D) {
+  if (s.DIN > s.D) {
     for (int f = tid; f < GW * 32; f += NT) {
       const int w = f / 32, n = f % 32;
       const int64_t c = c0 + w;
@@ -957,17 +970,16 @@ __device__ void gm_stage(const GArgs& a, const GL& g, float* L, int tid, int64_t
 }
 
 // x[k][n] of the wave's row and item n (0 past din)
-__device__ __forceinline__ float gm_x(const GArgs& a, const GL& g, const float* L, int w, int n,
-                                      int k) {
-  if (k < a.D) return L[g.o_hs + n * g.HD + k] * L[g.o_ts + w * a.D + k];
-  if (k < a.DIN) return L[g.o_fs + (w * 32 + n) * 4 + (k - a.D)];
+__device__ __forceinline__ float gm_x(const GS& s, const GL& g, const float* L, int w, int n, int k) {
+  if (k < s.D) return L[g.o_hs + n * g.HD + k] * L[g.o_ts + w * s.D + k];
+  if (k < s.DIN) return L[g.o_fs + (w * 32 + n) * 4 + (k - s.D)];
   return 0.f;
 }
 
 // Forward of the wave's 32 pairs (row c, items j0 + n): acc[hb] = dropout(b1 + W1 x) in the
 // 32x32 C layout (rows = hidden units, columns = pairs), the pair's h . t and attention logit.
 template <int HBM>
-__device__ __forceinline__ void gm_pair_forward(const GArgs& a, const GL& g, const float* L, int w,
+__device__ __forceinline__ void gm_pair_forward(const GArgs& a, const GS& s, const GL& g, const float* L, int w,
                                                 int lane, int64_t c, int64_t j0, floatx16 (&acc)[HBM],
                                                 float& sdot, float& alogit) {
   const int hh = lane >> 5, n = lane & 31;
@@ -976,10 +988,11 @@ __device__ __forceinline__ void gm_pair_forward(const GArgs& a, const GL& g, con
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[hb][r] = hb < g.HB ? L[g.o_b1 + crow(hb, r, hh)] : 0.f;
   float sp = 0.f;
+#pragma unroll
   for (int t = 0; t < g.DINP / 2; ++t) {
     const int k = 2 * t + hh;
-    const float x = gm_x(a, g, L, w, n, k);
-    if (k < a.D) sp += x;
+    const float x = gm_x(s, g, L, w, n, k);
+    if (k < s.D) sp += x;
 #pragma unroll
     for (int hb = 0; hb < HBM; ++hb)
       if (hb < g.HB) acc[hb] = mfma(L[g.o_w1 + (32 * hb + n) * g.Q + k], x, acc[hb]);
@@ -1008,22 +1021,23 @@ __device__ __forceinline__ float half_sum(float v) {
   return v;
 }
 
-template <int HBM>
+template <int HBM, int DC = 0, int HC = 0, int XC = 0>
 __global__ void __launch_bounds__(GW * 64)
 gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
   extern __shared__ float4 glds4[];
   float* L = reinterpret_cast<float*>(glds4);
-  const GL g(a.D, a.H, a.DIN);
+  const GS s = make_gs<DC, HC, XC>(a);
+  const GL g(s.D, s.H, s.DIN);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
   const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
   const int64_t j0 = int64_t(blockIdx.y) * 32;
   const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
-  gm_stage(a, g, L, tid, c0, j0, nj);
+  gm_stage(a, s, g, L, tid, c0, j0, nj);
   __syncthreads();
   if (c >= a.b) return;   // no barriers below
   floatx16 acc[HBM];
   float sdot, at;
-  gm_pair_forward<HBM>(a, g, L, w, lane, c, j0, acc, sdot, at);
+  gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
   float e = 0.f;
   if (n < nj) e = expf(at) * (a.hist[j0 + n] != a.target[c] ? 1.f : 0.f);   // model.py:74-78
   const float S = half_sum(e), N = half_sum(e * sdot);
@@ -1033,21 +1047,22 @@ gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
   }
 }
 
-template <int HBM>
+template <int HBM, int DC = 0, int HC = 0, int XC = 0>
 __global__ void __launch_bounds__(GW * 64, 1)
 gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
                    const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows) {
   if (bad_rows && *bad_rows) return;   // fused step on a NaN batch: no update (see train_loss)
   extern __shared__ float4 glds4[];
   float* L = reinterpret_cast<float*>(glds4);
-  const GL g(a.D, a.H, a.DIN);
+  const GS s = make_gs<DC, HC, XC>(a);
+  const GL g(s.D, s.H, s.DIN);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31, hh = lane >> 5;
   const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
   const bool live = c < a.b;
   const int64_t j0 = int64_t(blockIdx.y) * 32;
   const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
-  gm_stage(a, g, L, tid, c0, j0, nj);
-  for (int f = tid; f < 32 * a.D; f += GW * 64) L[g.o_gh + f] = 0.f;
+  gm_stage(a, s, g, L, tid, c0, j0, nj);
+  for (int f = tid; f < 32 * s.D; f += GW * 64) L[g.o_gh + f] = 0.f;
   for (int f = tid; f < 2 * g.HP32 + 8; f += GW * 64) L[g.o_gb + f] = 0.f;
   __syncthreads();
 
@@ -1057,7 +1072,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   const int64_t tgt = live ? a.target[c] : -1;
   float e = 0.f;
   if (live) {
-    gm_pair_forward<HBM>(a, g, L, w, lane, c, j0, acc, sdot, at);
+    gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
     if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
   } else {
 #pragma unroll
@@ -1100,7 +1115,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   // ---- dx = W1^T du (K-step (hb, r) = hidden unit crow(hb, r, hh): du straight from acc)
   constexpr int DBM = 4;
   floatx16 dx[DBM];
-  const int DB = (a.D + 31) / 32;
+  const int DB = (s.D + 31) / 32;
 #pragma unroll
   for (int q = 0; q < DBM; ++q)
 #pragma unroll
@@ -1117,9 +1132,9 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
 #pragma unroll
       for (int q = 0; q < DBM; ++q)
         if (q < DB) dx[q] = mfma(wrow[32 * q + n], du, dx[q]);
-      if (a.DIN > a.D) {
-        df0 = fmaf(wrow[a.D], du, df0);
-        df1 = fmaf(wrow[a.D + 1], du, df1);
+      if (s.DIN > s.D) {
+        df0 = fmaf(wrow[s.D], du, df0);
+        df1 = fmaf(wrow[s.D + 1], du, df1);
       }
     }
   }
@@ -1135,20 +1150,20 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     for (int r = 0; r < 16; ++r) {
       const int d = 32 * q + crow(0, r, hh);
       vt[r] = 0.f;
-      if (d < a.D && live && n < nj) {
+      if (d < s.D && live && n < nj) {
         const float rv = dx[q][r] + ds;
-        atomicAdd(&L[g.o_gh + n * a.D + d], rv * L[g.o_ts + w * a.D + d]);
+        atomicAdd(&L[g.o_gh + n * s.D + d], rv * L[g.o_ts + w * s.D + d]);
         vt[r] = rv * L[g.o_hs + n * g.HD + d];
       }
     }
     const float tt = half_reduce_scatter<16>(vt, lane);
     const int d = 32 * q + crow(0, n >> 1, hh);
-    if ((n & 1) == 0 && live && d < a.D) {
+    if ((n & 1) == 0 && live && d < s.D) {
       if (d < a.IDIM) unsafeAtomicAdd(&gr.et[tgt * a.IDIM + d], tt);
       else unsafeAtomicAdd(&gr.er[a.treg[c] * a.RDIM + (d - a.IDIM)], tt);
     }
   }
-  if (a.DIN > a.D) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the wave's pairs
+  if (s.DIN > s.D) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the wave's pairs
     df0 += __shfl_xor(df0, 32);
     df1 += __shfl_xor(df1, 32);
     float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1185,7 +1200,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         for (int r = 0; r < 16; ++r)
           if (hb < g.HB) L[g.o_su + n * g.UP + crow(hb, r, hh)] = acc[hb][r];
       for (int d = hh; d < g.DBX * 32; d += 2)
-        L[g.o_sx + n * g.XP + d] = (live && n < nj) ? gm_x(a, g, L, w, n, d) : 0.f;
+        L[g.o_sx + n * g.XP + d] = (live && n < nj) ? gm_x(s, g, L, w, n, d) : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -1210,16 +1225,16 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int i = 32 * ib + crow(0, r, hh), d = 32 * xb + n;
-      if (i < a.H && d < a.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * a.DIN + d], gw[q][r]);
+      if (i < s.H && d < s.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * s.DIN + d], gw[q][r]);
     }
   }
-  for (int i = tid; i < a.H; i += GW * 64) {
+  for (int i = tid; i < s.H; i += GW * 64) {
     unsafeAtomicAdd(&gr.b1[i], L[g.o_gb + i]);
     unsafeAtomicAdd(&gr.w2[i], L[g.o_gw + i]);
   }
-  if (a.DIN > a.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], L[g.o_gd + tid]);
-  for (int f = tid; f < nj * a.D; f += GW * 64) {
-    const int jj = f / a.D, d = f % a.D;
+  if (s.DIN > s.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], L[g.o_gd + tid]);
+  for (int f = tid; f < nj * s.D; f += GW * 64) {
+    const int jj = f / s.D, d = f % s.D;
     const int64_t j = j0 + jj;
     if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], L[g.o_gh + f]);
     else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], L[g.o_gh + f]);
@@ -1426,11 +1441,27 @@ size_t g_workspace(int64_t b, int64_t n) {
   return size_t(2 * ns * b) * sizeof(float);
 }
 
+// The compile-time instantiations of the general kernels: (D, H, extra input dims). Other shapes
+// run the runtime-shaped <HBM> kernels.
+#define NAIS_GM_SHAPES(X) X(4, 128, 128, 0) X(4, 128, 128, 2) X(2, 64, 64, 0) X(2, 64, 64, 2)
+// the backward at D = 128 with the 2 distance inputs spills (256 VGPRs + 36): runtime-shaped there
+#define NAIS_GM_SHAPES_BWD(X) X(4, 128, 128, 0) X(2, 64, 64, 0) X(2, 64, 64, 2)
+
 int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
   const size_t lds = g_lds_bytes(a, false);
-  static bool once = (set_lds(gm_forward_kernel<4>, 160 * 1024), set_lds(gm_forward_kernel<2>, 160 * 1024), true);
+#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_forward_kernel<HBM, DC, HC, XC>, 160 * 1024),
+  static bool once = (NAIS_GM_SHAPES(NAIS_GM_LDS) set_lds(gm_forward_kernel<4>, 160 * 1024),
+                      set_lds(gm_forward_kernel<2>, 160 * 1024), true);
+#undef NAIS_GM_LDS
   (void)once;
   dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+#define NAIS_GM_FWD(HBM, DC, HC, XC)                                                        \
+  if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
+    hipLaunchKernelGGL((gm_forward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, Sp, Np); \
+    return nais_internal_check_launch("gm_forward_kernel");                                \
+  }
+  NAIS_GM_SHAPES(NAIS_GM_FWD)
+#undef NAIS_GM_FWD
   if (a.H > 64) hipLaunchKernelGGL(gm_forward_kernel<4>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
   else hipLaunchKernelGGL(gm_forward_kernel<2>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
   return nais_internal_check_launch("gm_forward_kernel");
@@ -1439,9 +1470,20 @@ int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
 int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
                const GGrads& g, hipStream_t st, const int32_t* bad_rows = nullptr) {
   const size_t lds = g_lds_bytes(a, true);
-  static bool once = (set_lds(gm_backward_kernel<4>, 160 * 1024), set_lds(gm_backward_kernel<2>, 160 * 1024), true);
+#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_backward_kernel<HBM, DC, HC, XC>, 160 * 1024),
+  static bool once = (NAIS_GM_SHAPES_BWD(NAIS_GM_LDS) set_lds(gm_backward_kernel<4>, 160 * 1024),
+                      set_lds(gm_backward_kernel<2>, 160 * 1024), true);
+#undef NAIS_GM_LDS
   (void)once;
   dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+#define NAIS_GM_BWD(HBM, DC, HC, XC)                                                        \
+  if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
+    hipLaunchKernelGGL((gm_backward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, saved, \
+                       pred, gpred, g, bad_rows);                                          \
+    return nais_internal_check_launch("gm_backward_kernel");                               \
+  }
+  NAIS_GM_SHAPES_BWD(NAIS_GM_BWD)
+#undef NAIS_GM_BWD
   if (a.H > 64)
     hipLaunchKernelGGL(gm_backward_kernel<4>, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g, bad_rows);
   else

@@ -144,7 +144,8 @@ def distributed_topk(model, train_matrix, num_users, k, group=None, **kw):
     model.eval()
     csr = device_csr(train_matrix, model._check_device())
     P = model._item_tables()[0].shape[0]
-    if kw.get("prior") is None and distributed_plan(csr, num_users, P, k, world, model) == "pairs":
+    if distributed_plan(csr, num_users, P, k, world, model) == "pairs" and not (
+            kw.get("prior") is not None and model._pairs_only):
         return distributed_topk_pairs(model, csr, range(num_users), k, group=group, **kw)
     mine = shard_users(csr.hist_len[:num_users], P, world)[rank]
     ids, sc = score_topk(model, csr, mine, k, **kw)
@@ -173,7 +174,12 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     a local top-k -- then one all_gather of the [n, k] blocks and a merge by nais_topk_rows over
     the world*k candidates. Ranks own ascending id ranges, so the merge's (score desc, position
     asc) order is the global (score desc, POI id asc). Every user needs k candidates in every
-    column block (checked; otherwise raises ValueError -- use the user-sharded path)."""
+    column block (checked; otherwise raises ValueError -- use the user-sharded path).
+
+    With `prior` = (a, b, alpha, poi_coords) (run.py:537-539): each rank blends its columns with
+    the whole catalog's max G (a MAX all-reduce per user inside _score_topk_pairs), the lists carry
+    their f64 blended scores, and the merge ranks on those (nais_topk_merge_f64) -- the ranking of
+    the single-process blend, bit for bit."""
     import torch.distributed as dist
     from . import _capi
     from .catalog import _score_topk_pairs, device_csr
@@ -187,6 +193,20 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
         raise ValueError("a column block has fewer than k candidates for some user "
                          "(use the user-sharded path, distributed_topk falls back to it)")
     c0, c1 = column_blocks(P, world)[rank]
+    prior = kw.get("prior")
+    if prior is not None:
+        ids, sc, keys = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
+                                          kw.get("latlon_mat"), None, force=True, cols=(c0, c1),
+                                          events=events, prior=prior,
+                                          group=(group if group is not None else dist.group.WORLD)
+                                          if world > 1 else None, return_keys=True)
+        if world == 1:
+            return ids, sc
+        gi = torch.empty(world, n, k, dtype=torch.int64, device=dev)
+        gk = torch.empty(world, n, k, dtype=torch.float64, device=dev)
+        _all_gather_blocks(gi, ids, group)
+        _all_gather_blocks(gk, keys, group)
+        return merge_topk_f64(gi, gk, k)
     ids, sc = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
                                 kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events)
     if world == 1:
@@ -200,6 +220,49 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
         dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
         dist.all_gather_into_tensor(gs, sc.contiguous(), group=group)
     return merge_topk(gi, gs, k)
+
+
+def agree_min(value, device, group=None):
+    """The smallest `value` over the ranks (an int; e.g. users per pass, so that every rank makes
+    the same passes and hence the same per-pass collectives)."""
+    import torch.distributed as dist
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item())
+
+
+def allreduce_gmax(gmax_bits, group=None):
+    """In place: each user's max G over every rank's columns. gmax_bits holds the u64 bit patterns
+    of non-negative doubles (nais_pair_prior_gather), which order like the doubles, so an int64 MAX
+    all-reduce is the float64 max (run.py:55-59's max over the whole catalog)."""
+    import torch.distributed as dist
+    dist.all_reduce(gmax_bits, op=dist.ReduceOp.MAX, group=group)
+    return gmax_bits
+
+
+def _all_gather_blocks(out, block, group):
+    """out[world, ...] <- every rank's `block` (gloo: list all_gather; RCCL: one tensor)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        dist.all_gather(list(out.unbind(0)), block.contiguous(), group=group)
+    else:
+        dist.all_gather_into_tensor(out, block.contiguous(), group=group)
+
+
+def merge_topk_f64(ids, keys, k):
+    """[world, n, k] per-column-block lists with f64 ranking keys (global POI ids, -1 = padding)
+    -> the [n, k] global top-k by (key desc, id asc), NaN first (nais_topk_merge_f64)."""
+    from . import _capi
+    world, n, _ = ids.shape
+    dev = ids.device
+    cand_k = keys.permute(1, 0, 2).reshape(n, world * k).contiguous()
+    cand_i = ids.permute(1, 0, 2).reshape(n, world * k).contiguous()
+    out_i = torch.empty(n, k, dtype=torch.int64, device=dev)
+    out_s = torch.empty(n, k, dtype=torch.float32, device=dev)
+    _capi.check(_capi.load().nais_topk_merge_f64(cand_k.data_ptr(), cand_i.data_ptr(), n, world * k, k,
+                                                 out_i.data_ptr(), out_s.data_ptr(), None,
+                                                 _capi.stream_handle(dev)), "nais_topk_merge_f64")
+    return out_i, out_s
 
 
 def merge_topk(ids, scores, k):

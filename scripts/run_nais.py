@@ -23,7 +23,8 @@ from poi_recommendation_models_amd.trainer import NAISTrainer  # noqa: E402
 
 
 class Args:
-    """run.py:830-844 (factor_num / hidden_dim 64: the training kernels' current limit)."""
+    """run.py:830-844, at factor_num = hidden_dim = 64 (the fused training kernels' shape; the
+    reference's default 128 runs the general kernels, DESIGN.md "General training kernels")."""
     lr = 0.01
     lamda = 0.0
     epochs = 50

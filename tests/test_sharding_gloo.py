@@ -326,3 +326,110 @@ def test_column_sharded_merge_world3_p_not_divisible():
         for rank, _, ids, sc in res:
             np.testing.assert_array_equal(ids[u], rid)
             np.testing.assert_array_equal(sc[u], rsc)
+
+
+def _fake_merge_f64(keys, ids, n, m, k, out_ids, out_scores, out_keys, stream):
+    """nais_topk_merge_f64 (include/nais.h) restated in numpy over raw CPU pointers."""
+    import ctypes
+    kk = np.ctypeslib.as_array((ctypes.c_double * (n * m)).from_address(keys)).reshape(n, m)
+    ii = np.ctypeslib.as_array((ctypes.c_int64 * (n * m)).from_address(ids)).reshape(n, m)
+    oi = np.ctypeslib.as_array((ctypes.c_int64 * (n * k)).from_address(out_ids)).reshape(n, k)
+    os_ = np.ctypeslib.as_array((ctypes.c_float * (n * k)).from_address(out_scores)).reshape(n, k)
+    for r in range(n):
+        ok = ii[r] >= 0
+        i, t = nais_oracle.topk_ids(ii[r][ok], kk[r][ok], k)
+        oi[r, :len(i)], os_[r, :len(i)] = i, t.astype(np.float32)
+        oi[r, len(i):], os_[r, len(i):] = -1, np.nan
+    return 0
+
+
+PRIOR = (0.052, -1.37, 0.2)
+
+
+def _prior_case():
+    from poi_recommendation_models_amd.synthetic import init_nais_params
+    P, U = 151, 6
+    p = init_nais_params(P, 16, 16, seed=41, emb_std=0.3, bias_std=0.1)
+    rng = np.random.default_rng(42)
+    coords = np.stack([40.7 + rng.random(P) * 0.2, -74.0 + rng.random(P) * 0.2], 1)
+    hist = [np.sort(rng.choice(P, int(rng.integers(1, 12)), replace=False)) for _ in range(U)]
+    return P, U, p, coords, hist
+
+
+def _blend_rows(p, coords, hist, P, cols):
+    """(candidate ids in [c0, c1), f32 score, f64 G) of one user (oracle restatements)."""
+    from oracle import powerlaw_oracle
+    cand, s = nais_oracle.catalog_scores_basic(p, hist, P)
+    keep = (cand >= cols[0]) & (cand < cols[1])
+    cl = [tuple(c) for c in coords.tolist()]
+    G = np.array([powerlaw_oracle.predict(PRIOR[0], PRIOR[1], cl, hist, int(c)) for c in cand[keep]])
+    return cand[keep], s[keep], G
+
+
+def _worker_prior(rank, world, port, q):
+    """The column-sharded prior's collectives (sharding.allreduce_gmax, the product code) and its
+    f64 merge (sharding.merge_topk_f64 over nais_topk_merge_f64 restated in numpy): each rank blends
+    its columns with the all-reduced max G, and the merged lists equal the single-process blend."""
+    import torch.distributed as dist
+    from oracle import powerlaw_oracle
+    from poi_recommendation_models_amd import _capi, sharding
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, U, p, coords, hist = _prior_case()
+    K = 10
+    c0, c1 = sharding.column_blocks(P, world)[rank]
+    rows = [_blend_rows(p, coords, h, P, (c0, c1)) for h in hist]
+    gmax = torch.tensor([max(g.max(), 0.0) for _, _, g in rows], dtype=torch.float64).view(torch.int64)
+    local_max = gmax.view(torch.float64).clone()
+    sharding.allreduce_gmax(gmax)
+    gm = gmax.view(torch.float64).numpy()
+    ids, keys = [], []
+    for u, (cand, s, G) in enumerate(rows):
+        gn = G / gm[u] if gm[u] != 0 else G
+        b = powerlaw_oracle.blend(s, gn, PRIOR[2])
+        i, t = nais_oracle.topk_ids(cand, b, K)
+        ids.append(i)
+        keys.append(t)
+    gi = torch.empty(world, U, K, dtype=torch.int64)
+    gk = torch.empty(world, U, K, dtype=torch.float64)
+    sharding._all_gather_blocks(gi, torch.as_tensor(np.array(ids, dtype=np.int64)), None)
+    sharding._all_gather_blocks(gk, torch.as_tensor(np.array(keys, dtype=np.float64)), None)
+
+    class Lib:
+        nais_topk_merge_f64 = staticmethod(_fake_merge_f64)
+    _capi.load = lambda *a: Lib()
+    _capi.stream_handle = lambda dev: None
+    mi, ms = sharding.merge_topk_f64(gi, gk, K)
+    q.put((rank, local_max.numpy(), gm.copy(), mi.numpy(), ms.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_column_sharded_prior_max_allreduce_world2():
+    """the prior over column shards normalises by the max G of the WHOLE
+    catalog (MAX all-reduce of each user's per-shard max) and merges on the f64 blended score:
+    the merged top-k equals the single-process blended top-k (run.py:537-539) exactly."""
+    from oracle import powerlaw_oracle
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_prior, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    P, U, p, coords, hist = _prior_case()
+    K = 10
+    np.testing.assert_array_equal(res[0][2], np.maximum(res[0][1], res[1][1]))   # the global max
+    assert np.any(res[0][1] != res[1][1])             # the shards' own maxima do differ
+    for u in range(U):
+        cand, s, G = _blend_rows(p, coords, hist[u], P, (0, P))
+        b = powerlaw_oracle.blend(s, np.asarray(powerlaw_oracle.normalize(list(G))), PRIOR[2])
+        rid, rsc = nais_oracle.topk_ids(cand, b, K)
+        for rank, _, gm, mi, ms in res:
+            assert gm[u] == G.max()
+            np.testing.assert_array_equal(mi[u], rid)
+            np.testing.assert_array_equal(ms[u], rsc.astype(np.float32))
