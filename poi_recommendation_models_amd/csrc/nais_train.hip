@@ -865,6 +865,21 @@ __device__ __forceinline__ float rl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// The general backward runs one unit per workgroup (persistent = 1 keeps W1 staged across units but
+// spills at D = H = 128: the A/B knob).
+#ifndef NAIS_GM_BWD_PERSIST
+#define NAIS_GM_BWD_PERSIST 0
+#endif
+constexpr bool GM_BWD_PERSIST = NAIS_GM_BWD_PERSIST;
+
+// The LDS base as an opaque per-iteration value: inside the persistent unit loops, reads of the
+// loop-invariant W1 image would otherwise be hoisted out of the loop into (spilled) registers.
+__device__ __forceinline__ float* opaque_lds(float* L) {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return L + z;
+}
+
 // element d of the full history / target row
 __device__ __forceinline__ float hfull(const GArgs& a, int64_t j, int d) {
   if (d >= a.D) return 0.f;
@@ -915,20 +930,21 @@ struct GL {
     o_ts = o_hs + 32 * HD;              // [GW][D]  full target rows of the workgroup
     o_fs = o_ts + GW * D;               // [GW][32][4] f0, f1, 100 lat, 100 lng (region_distance)
     fwd = o_fs + GW * 32 * 4;
-    o_gh = fwd;                         // [32][D]  history-row grads of the slice
-    o_su = o_gh + 32 * D;               // [32][UP] du^T stage (one wave's pairs)
-    o_sx = o_su + 32 * UP;              // [32][XP] x stage
-    o_gb = o_sx + 32 * XP;              // [HP32] db1
+    o_gh = fwd;                         // [32][HD] history-row grads of the slice (odd pitch:
+                                        //          the 32 lanes' items hit distinct banks)
+    o_su = o_gh + 32 * HD;              // [2][32][UP] du^T stages (one wave's pairs each; double
+                                        //             buffered: the next wave stages while the
+                                        //             current one's are consumed)
+    o_sx = o_su + 32 * UP;              // the second du stage
+    o_gb = o_sx + 32 * UP;              // [HP32] db1
     o_gw = o_gb + HP32;                 // [HP32] dw2
     o_gd = o_gw + HP32;                 // [8]    dist_layer dw | db
     bwd = o_gd + 8;
   }
 };
 
-// stage W1 (row-major, pitch Q, zero padded), b1, w2, the slice's full history rows and the
-// workgroup's full target rows (+ the distance features of every (row, item) pair)
-__device__ __forceinline__ void gm_stage(const GArgs& a, const GS& s, const GL& g, float* L, int tid,
-                                         int64_t c0, int64_t j0, int nj) {
+// stage W1 (row-major, pitch Q, zero padded), b1, w2 -- once per (persistent) workgroup
+__device__ __forceinline__ void gm_stage_w(const GArgs& a, const GS& s, const GL& g, float* L, int tid) {
   constexpr int NT = GW * 64;
   for (int f = tid; f < g.HP32 * g.Q; f += NT) {
     const int i = f / g.Q, k = f % g.Q;
@@ -938,6 +954,12 @@ __device__ __forceinline__ void gm_stage(const GArgs& a, const GS& s, const GL& 
     L[g.o_b1 + i] = i < s.H ? a.b1[i] : 0.f;
     L[g.o_w2 + i] = i < s.H ? a.w2[i] : 0.f;
   }
+}
+
+// one work unit's operands: the slice's full history rows, the row tile's full target rows
+__device__ __forceinline__ void gm_stage(const GArgs& a, const GS& s, const GL& g, float* L, int tid,
+                                         int64_t c0, int64_t j0, int nj) {
+  constexpr int NT = GW * 64;
   for (int f = tid; f < 32 * g.HD; f += NT) {
     const int n = f / g.HD, d = f % g.HD;
     L[g.o_hs + f] = (n < nj && d < s.D) ? hfull(a, j0 + n, d) : 0.f;
@@ -1025,25 +1047,34 @@ template <int HBM, int DC = 0, int HC = 0, int XC = 0>
 __global__ void __launch_bounds__(GW * 64)
 gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
   extern __shared__ float4 glds4[];
-  float* L = reinterpret_cast<float*>(glds4);
+  float* Lb = reinterpret_cast<float*>(glds4);
   const GS s = make_gs<DC, HC, XC>(a);
   const GL g(s.D, s.H, s.DIN);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
-  const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
-  const int64_t j0 = int64_t(blockIdx.y) * 32;
-  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
-  gm_stage(a, s, g, L, tid, c0, j0, nj);
-  __syncthreads();
-  if (c >= a.b) return;   // no barriers below
-  floatx16 acc[HBM];
-  float sdot, at;
-  gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
-  float e = 0.f;
-  if (n < nj) e = expf(at) * (a.hist[j0 + n] != a.target[c] ? 1.f : 0.f);   // model.py:74-78
-  const float S = half_sum(e), N = half_sum(e * sdot);
-  if (lane == 0) {
-    Sp[int64_t(blockIdx.y) * a.b + c] = S;
-    Np[int64_t(blockIdx.y) * a.b + c] = N;
+  // persistent: W1 staged once, then work units (row tile of GW rows, slice of 32 items), row
+  // tile fastest, strided over the grid
+  gm_stage_w(a, s, g, Lb, tid);
+  const int64_t nrt = (a.b + GW - 1) / GW, units = nrt * ((a.n + 31) / 32);
+  for (int64_t un = blockIdx.x; un < units; un += gridDim.x) {
+    const int64_t sl = un / nrt, c0 = (un % nrt) * GW, c = c0 + w;
+    const int64_t j0 = sl * 32;
+    const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+    __syncthreads();   // the previous unit's operand reads are done
+    float* L = opaque_lds(Lb);
+    gm_stage(a, s, g, L, tid, c0, j0, nj);
+    __syncthreads();
+    if (c < a.b) {
+      floatx16 acc[HBM];
+      float sdot, at;
+      gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
+      float e = 0.f;
+      if (n < nj) e = expf(at) * (a.hist[j0 + n] != a.target[c] ? 1.f : 0.f);   // model.py:74-78
+      const float S = half_sum(e), N = half_sum(e * sdot);
+      if (lane == 0) {
+        Sp[sl * a.b + c] = S;
+        Np[sl * a.b + c] = N;
+      }
+    }
   }
 }
 
@@ -1053,192 +1084,217 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
                    const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows) {
   if (bad_rows && *bad_rows) return;   // fused step on a NaN batch: no update (see train_loss)
   extern __shared__ float4 glds4[];
-  float* L = reinterpret_cast<float*>(glds4);
+  float* Lb = reinterpret_cast<float*>(glds4);
   const GS s = make_gs<DC, HC, XC>(a);
   const GL g(s.D, s.H, s.DIN);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31, hh = lane >> 5;
-  const int64_t c0 = int64_t(blockIdx.x) * GW, c = c0 + w;
-  const bool live = c < a.b;
-  const int64_t j0 = int64_t(blockIdx.y) * 32;
-  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
-  gm_stage(a, s, g, L, tid, c0, j0, nj);
-  for (int f = tid; f < 32 * s.D; f += GW * 64) L[g.o_gh + f] = 0.f;
-  for (int f = tid; f < 2 * g.HP32 + 8; f += GW * 64) L[g.o_gb + f] = 0.f;
-  __syncthreads();
-
-  // ---- recompute the forward, then du in place (C layout)
-  floatx16 acc[HBM];
-  float sdot = 0.f, at = 0.f;
-  const int64_t tgt = live ? a.target[c] : -1;
-  float e = 0.f;
-  if (live) {
-    gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
-    if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
-  } else {
-#pragma unroll
-    for (int hb = 0; hb < HBM; ++hb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[hb][r] = 0.f;
-  }
-  float ds = 0.f, da = 0.f;
-  if (live) {
-    const float S = saved[c], N = saved[a.b + c], pc = pred[c];
-    const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid)
-    const float Sb = (a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta);
-    ds = gl / Sb * e;                                           // dlogit / ds_cj
-    da = ds * (sdot - a.beta * N / S);                          // dlogit / da_cj
-  }
-  const uint32_t key = (live && a.drop.on) ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
-  // du in place; db1 / dw2 as sums over the 32 pairs of each half (reduce-scatter), LDS atomics
-#pragma unroll
-  for (int hb = 0; hb < HBM; ++hb) {
-    if (hb >= g.HB) continue;
-    float vb[16], vz[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = crow(hb, r, hh);
-      const float v = acc[hb][r];
-      const float m = a.drop.on ? a.drop.factor(key, i) : 1.f;
-      const float du = v > 0.f ? da * L[g.o_w2 + i] * m : 0.f;   // ReLU + dropout backward
-      acc[hb][r] = du;
-      vb[r] = du;
-      vz[r] = da * nais_relu(v);
-    }
-    const float tb = half_reduce_scatter<16>(vb, lane);
-    const float tz = half_reduce_scatter<16>(vz, lane);
-    if ((n & 1) == 0 && live) {
-      const int i = crow(hb, n >> 1, hh);
-      atomicAdd(&L[g.o_gb + i], tb);
-      atomicAdd(&L[g.o_gw + i], tz);
-    }
-  }
-  // ---- dx = W1^T du (K-step (hb, r) = hidden unit crow(hb, r, hh): du straight from acc)
-  constexpr int DBM = 4;
-  floatx16 dx[DBM];
-  const int DB = (s.D + 31) / 32;
-#pragma unroll
-  for (int q = 0; q < DBM; ++q)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dx[q][r] = 0.f;
-  float df0 = 0.f, df1 = 0.f;
-#pragma unroll
-  for (int hb = 0; hb < HBM; ++hb) {
-    if (hb >= g.HB) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = crow(hb, r, hh);
-      const float du = acc[hb][r];
-      const float* wrow = L + g.o_w1 + i * g.Q;
-#pragma unroll
-      for (int q = 0; q < DBM; ++q)
-        if (q < DB) dx[q] = mfma(wrow[32 * q + n], du, dx[q]);
-      if (s.DIN > s.D) {
-        df0 = fmaf(wrow[s.D], du, df0);
-        df1 = fmaf(wrow[s.D + 1], du, df1);
-      }
-    }
-  }
-  // ---- r = dx + ds: history-row grads (LDS atomics per item) and the target-row grad
-#pragma unroll
-  for (int q = 0; q < DBM; ++q) {
-    if (q >= DB) continue;
-    float vt[16];
-    // the lane holds dx[d][pair n] for the C-tile rows d = 32 q + crow(0, r, hh)
-    // (LDS atomics for the history-row grads: keeping r live until a per-wave round instead
-    // costs registers and measured slower, 0.84 vs 0.77 ms at D = H = 128)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = 32 * q + crow(0, r, hh);
-      vt[r] = 0.f;
-      if (d < s.D && live && n < nj) {
-        const float rv = dx[q][r] + ds;
-        atomicAdd(&L[g.o_gh + n * s.D + d], rv * L[g.o_ts + w * s.D + d]);
-        vt[r] = rv * L[g.o_hs + n * g.HD + d];
-      }
-    }
-    const float tt = half_reduce_scatter<16>(vt, lane);
-    const int d = 32 * q + crow(0, n >> 1, hh);
-    if ((n & 1) == 0 && live && d < s.D) {
-      if (d < a.IDIM) unsafeAtomicAdd(&gr.et[tgt * a.IDIM + d], tt);
-      else unsafeAtomicAdd(&gr.er[a.treg[c] * a.RDIM + (d - a.IDIM)], tt);
-    }
-  }
-  if (s.DIN > s.D) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the wave's pairs
-    df0 += __shfl_xor(df0, 32);
-    df1 += __shfl_xor(df1, 32);
-    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (live && n < nj && hh == 0) {
-      const float* fs = L + g.o_fs + (w * 32 + n) * 4;
-      const float q0 = df0 * fs[0] * (1.f - fs[0]), q1 = df1 * fs[1] * (1.f - fs[1]);
-      qv[0] = q0 * fs[2];
-      qv[1] = q0 * fs[3];
-      qv[2] = q1 * fs[2];
-      qv[3] = q1 * fs[3];
-      qv[4] = q0;
-      qv[5] = q1;
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const float t = half_sum(qv[k]);
-      if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
-    }
-  }
-  // ---- dW1 = sum over the workgroup's pairs of du x^T: each wave's 32 pairs staged in turn,
-  // every wave accumulating the output tiles it owns (tiles w, w + GW, w + 2 GW)
-  constexpr int OWN = 3;
-  floatx16 gw[OWN];
-#pragma unroll
-  for (int q = 0; q < OWN; ++q)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) gw[q][r] = 0.f;
+  // persistent: W1 staged once and db1 / dw2 / dist_layer grads kept in LDS across all of the
+  // workgroup's units (row tile of GW rows, slice of 32 items), flushed once; the dW1 tiles and the
+  // history-row grads are flushed per unit (registers: the dW1 tiles are live in its last phase only)
+  gm_stage_w(a, s, g, Lb, tid);
+  for (int f = tid; f < 2 * g.HP32 + 8; f += GW * 64) Lb[g.o_gb + f] = 0.f;
   const int ntile = g.HB * g.DBX;
-  for (int rd = 0; rd < GW; ++rd) {
-    if (w == rd) {
-#pragma unroll
-      for (int hb = 0; hb < HBM; ++hb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (hb < g.HB) L[g.o_su + n * g.UP + crow(hb, r, hh)] = acc[hb][r];
-      for (int d = hh; d < g.DBX * 32; d += 2)
-        L[g.o_sx + n * g.XP + d] = (live && n < nj) ? gm_x(s, g, L, w, n, d) : 0.f;
-    }
+  const int64_t nrt = (a.b + GW - 1) / GW, units = nrt * ((a.n + 31) / 32);
+  // one unit: the loop body of the persistent form (a lambda, so that the one-unit-per-workgroup
+  // launch below carries no loop state -- the persistent loop spills the D = H = 128 backward)
+  auto unit = [&](int64_t un) {
+    const int64_t sl = un / nrt, c0 = (un % nrt) * GW, c = c0 + w;
+    const bool live = c < a.b;
+    const int64_t j0 = sl * 32;
+    const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+    __syncthreads();   // the previous unit's operand reads and grad flush are done
+    float* L = opaque_lds(Lb);
+    gm_stage(a, s, g, L, tid, c0, j0, nj);
+    for (int f = tid; f < 32 * g.HD; f += GW * 64) L[g.o_gh + f] = 0.f;
     __syncthreads();
+
+    // ---- recompute the forward, then du in place (C layout)
+    floatx16 acc[HBM];
+    float sdot = 0.f, at = 0.f;
+    const int64_t tgt = live ? a.target[c] : -1;
+    float e = 0.f;
+    if (live) {
+      gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
+      if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
+    } else {
+  #pragma unroll
+      for (int hb = 0; hb < HBM; ++hb)
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) acc[hb][r] = 0.f;
+    }
+    float ds = 0.f, da = 0.f;
+    if (live) {
+      const float S = saved[c], N = saved[a.b + c], pc = pred[c];
+      const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid)
+      const float Sb = (a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta);
+      ds = gl / Sb * e;                                           // dlogit / ds_cj
+      da = ds * (sdot - a.beta * N / S);                          // dlogit / da_cj
+    }
+    const uint32_t key = (live && a.drop.on) ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
+    // du in place; db1 / dw2 as sums over the 32 pairs of each half (reduce-scatter), LDS atomics
+  #pragma unroll
+    for (int hb = 0; hb < HBM; ++hb) {
+      if (hb >= g.HB) continue;
+      float vb[16], vz[16];
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = crow(hb, r, hh);
+        const float v = acc[hb][r];
+        const float m = a.drop.on ? a.drop.factor(key, i) : 1.f;
+        const float du = v > 0.f ? da * L[g.o_w2 + i] * m : 0.f;   // ReLU + dropout backward
+        acc[hb][r] = du;
+        vb[r] = du;
+        vz[r] = da * nais_relu(v);
+      }
+      const float tb = half_reduce_scatter<16>(vb, lane);
+      const float tz = half_reduce_scatter<16>(vz, lane);
+      if ((n & 1) == 0 && live) {
+        const int i = crow(hb, n >> 1, hh);
+        atomicAdd(&L[g.o_gb + i], tb);
+        atomicAdd(&L[g.o_gw + i], tz);
+      }
+    }
+    // ---- dx = W1^T du (K-step (hb, r) = hidden unit crow(hb, r, hh): du straight from acc)
+    constexpr int DBM = 4;
+    floatx16 dx[DBM];
+    const int DB = (s.D + 31) / 32;
+  #pragma unroll
+    for (int q = 0; q < DBM; ++q)
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) dx[q][r] = 0.f;
+    float df0 = 0.f, df1 = 0.f;
+  #pragma unroll
+    for (int hb = 0; hb < HBM; ++hb) {
+      if (hb >= g.HB) continue;
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = crow(hb, r, hh);
+        const float du = acc[hb][r];
+        const float* wrow = L + g.o_w1 + i * g.Q;
+  #pragma unroll
+        for (int q = 0; q < DBM; ++q)
+          if (q < DB) dx[q] = mfma(wrow[32 * q + n], du, dx[q]);
+        if (s.DIN > s.D) {
+          df0 = fmaf(wrow[s.D], du, df0);
+          df1 = fmaf(wrow[s.D + 1], du, df1);
+        }
+      }
+    }
+    // ---- r = dx + ds: history-row grads (LDS atomics per item) and the target-row grad
+  #pragma unroll
+    for (int q = 0; q < DBM; ++q) {
+      if (q >= DB) continue;
+      float vt[16];
+      // the lane holds dx[d][pair n] for the C-tile rows d = 32 q + crow(0, r, hh)
+      // (LDS atomics for the history-row grads: keeping r live until a per-wave round instead
+      // costs registers and measured slower, 0.84 vs 0.77 ms at D = H = 128)
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = 32 * q + crow(0, r, hh);
+        vt[r] = 0.f;
+        if (d < s.D && live && n < nj) {
+          const float rv = dx[q][r] + ds;
+          atomicAdd(&L[g.o_gh + n * g.HD + d], rv * L[g.o_ts + w * s.D + d]);
+          vt[r] = rv * L[g.o_hs + n * g.HD + d];
+        }
+      }
+      const float tt = half_reduce_scatter<16>(vt, lane);
+      const int d = 32 * q + crow(0, n >> 1, hh);
+      if ((n & 1) == 0 && live && d < s.D) {
+        if (d < a.IDIM) unsafeAtomicAdd(&gr.et[tgt * a.IDIM + d], tt);
+        else unsafeAtomicAdd(&gr.er[a.treg[c] * a.RDIM + (d - a.IDIM)], tt);
+      }
+    }
+    if (s.DIN > s.D) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the wave's pairs
+      df0 += __shfl_xor(df0, 32);
+      df1 += __shfl_xor(df1, 32);
+      float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (live && n < nj && hh == 0) {
+        const float* fs = L + g.o_fs + (w * 32 + n) * 4;
+        const float q0 = df0 * fs[0] * (1.f - fs[0]), q1 = df1 * fs[1] * (1.f - fs[1]);
+        qv[0] = q0 * fs[2];
+        qv[1] = q0 * fs[3];
+        qv[2] = q1 * fs[2];
+        qv[3] = q1 * fs[3];
+        qv[4] = q0;
+        qv[5] = q1;
+      }
+  #pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const float t = half_sum(qv[k]);
+        if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
+      }
+    }
+    constexpr int OWN = 3;
+    floatx16 gw[OWN];
 #pragma unroll
+    for (int q = 0; q < OWN; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gw[q][r] = 0.f;
+    // ---- dW1 = sum over the workgroup's pairs of du x^T: each wave's 32 pairs of du staged in
+    // turn (double-buffered: wave rd + 1 stages while every wave consumes wave rd's), x recomputed
+    // from the LDS rows by the consumers; every wave accumulates the output tiles it owns (tiles w,
+    // w + GW, w + 2 GW). One barrier per round.
+    const int ntile = g.HB * g.DBX;
+    auto stage_du = [&](int buf) {
+      float* dst = L + (buf ? g.o_sx : g.o_su) + n * g.UP;
+  #pragma unroll
+      for (int hb = 0; hb < HBM; ++hb)
+  #pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (hb < g.HB) dst[crow(hb, r, hh)] = acc[hb][r];
+    };
+    if (w == 0) stage_du(0);
+    __syncthreads();
+    for (int rd = 0; rd < GW; ++rd) {
+      if (rd + 1 < GW && w == rd + 1) stage_du((rd + 1) & 1);
+      const float* su = L + ((rd & 1) ? g.o_sx : g.o_su);
+  #pragma unroll
+      for (int q = 0; q < OWN; ++q) {
+        const int tile = w + q * GW;
+        if (tile >= ntile) continue;
+        const int ib = tile / g.DBX, xb = tile % g.DBX;
+  #pragma unroll 4
+        for (int t = 0; t < 16; ++t) {
+          const int p = 2 * t + hh;
+          gw[q] = mfma(su[p * g.UP + 32 * ib + n], gm_x(s, g, L, rd, p, 32 * xb + n), gw[q]);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- the unit's dW1 tiles
+  #pragma unroll
     for (int q = 0; q < OWN; ++q) {
       const int tile = w + q * GW;
       if (tile >= ntile) continue;
       const int ib = tile / g.DBX, xb = tile % g.DBX;
-#pragma unroll 4
-      for (int t = 0; t < 16; ++t) {
-        const int p = 2 * t + hh;
-        gw[q] = mfma(L[g.o_su + p * g.UP + 32 * ib + n], L[g.o_sx + p * g.XP + 32 * xb + n], gw[q]);
+  #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * ib + crow(0, r, hh), d = 32 * xb + n;
+        if (i < s.H && d < s.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * s.DIN + d], gw[q][r]);
       }
     }
-    __syncthreads();
-  }
-  // ---- flush: dW1 tiles, db1 / dw2, dist_layer, the slice's history-row grads
-#pragma unroll
-  for (int q = 0; q < OWN; ++q) {
-    const int tile = w + q * GW;
-    if (tile >= ntile) continue;
-    const int ib = tile / g.DBX, xb = tile % g.DBX;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = 32 * ib + crow(0, r, hh), d = 32 * xb + n;
-      if (i < s.H && d < s.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * s.DIN + d], gw[q][r]);
+    // ---- the unit's history-row grads (the last dW1 round's barrier ordered every LDS atomic)
+    for (int f = tid; f < nj * s.D; f += GW * 64) {
+      const int jj = f / s.D, d = f % s.D;
+      const int64_t j = j0 + jj;
+      const float v = L[g.o_gh + jj * g.HD + d];
+      if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], v);
+      else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], v);
     }
+  };
+  if constexpr (GM_BWD_PERSIST) {
+    for (int64_t un = blockIdx.x; un < units; un += gridDim.x) unit(un);
+  } else {
+    unit(blockIdx.x);
   }
+  // ---- flush (once per workgroup): db1 / dw2, dist_layer
+  __syncthreads();
   for (int i = tid; i < s.H; i += GW * 64) {
-    unsafeAtomicAdd(&gr.b1[i], L[g.o_gb + i]);
-    unsafeAtomicAdd(&gr.w2[i], L[g.o_gw + i]);
+    unsafeAtomicAdd(&gr.b1[i], Lb[g.o_gb + i]);
+    unsafeAtomicAdd(&gr.w2[i], Lb[g.o_gw + i]);
   }
-  if (s.DIN > s.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], L[g.o_gd + tid]);
-  for (int f = tid; f < nj * s.D; f += GW * 64) {
-    const int jj = f / s.D, d = f % s.D;
-    const int64_t j = j0 + jj;
-    if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], L[g.o_gh + f]);
-    else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], L[g.o_gh + f]);
-  }
+  if (s.DIN > s.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], Lb[g.o_gd + tid]);
 }
 
 size_t g_lds_bytes(const GArgs& a, bool backward) {
@@ -1441,6 +1497,17 @@ size_t g_workspace(int64_t b, int64_t n) {
   return size_t(2 * ns * b) * sizeof(float);
 }
 
+int device_cus() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return cus;
+  }();
+  return n;
+}
+
 // The compile-time instantiations of the general kernels: (D, H, extra input dims). Other shapes
 // run the runtime-shaped <HBM> kernels.
 #define NAIS_GM_SHAPES(X) X(4, 128, 128, 0) X(4, 128, 128, 2) X(2, 64, 64, 0) X(2, 64, 64, 2)
@@ -1454,7 +1521,9 @@ int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
                       set_lds(gm_forward_kernel<2>, 160 * 1024), true);
 #undef NAIS_GM_LDS
   (void)once;
-  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+  // persistent: one workgroup per CU (the LDS image holds one), units strided over the grid
+  const int64_t units = ((a.b + GW - 1) / GW) * ((a.n + 31) / 32);
+  dim3 grid((unsigned)std::min<int64_t>(units, device_cus()));
 #define NAIS_GM_FWD(HBM, DC, HC, XC)                                                        \
   if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
     hipLaunchKernelGGL((gm_forward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, Sp, Np); \
@@ -1475,7 +1544,8 @@ int g_backward(const GArgs& a, const float* saved, const float* pred, const floa
                       set_lds(gm_backward_kernel<2>, 160 * 1024), true);
 #undef NAIS_GM_LDS
   (void)once;
-  dim3 grid((unsigned)((a.b + GW - 1) / GW), (unsigned)((a.n + 31) / 32));
+  const int64_t units = ((a.b + GW - 1) / GW) * ((a.n + 31) / 32);
+  dim3 grid((unsigned)(GM_BWD_PERSIST ? std::min<int64_t>(units, device_cus()) : units));
 #define NAIS_GM_BWD(HBM, DC, HC, XC)                                                        \
   if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
     hipLaunchKernelGGL((gm_backward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, saved, \
