@@ -842,7 +842,10 @@ make_batch_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict_
 // and adds them to the caller's gradients with global atomics; target-row grads go straight from
 // registers.
 // ---------------------------------------------------------------------------------------------
-constexpr int GW = 8;                 // rows (waves) per workgroup
+#ifndef NAIS_GM_GW
+#define NAIS_GM_GW 12   // 3 waves per SIMD (153-167 VGPRs); A/B vs 8: step 0.567 -> 0.530 ms at D = H = 128
+#endif
+constexpr int GW = NAIS_GM_GW;        // rows (waves) per workgroup
 constexpr int G_MAX_D = 128, G_MAX_H = 128, G_MAX_DIN = G_MAX_D + 2;
 
 struct GArgs {
@@ -855,6 +858,10 @@ struct GArgs {
   float beta, dscale;
   int js;
   Drop drop;
+  // fused step only (nais_train_step): the forward's post-dropout u (the wave's accumulator
+  // registers), s = h . t and the attention logit of every pair, read back by the backward instead
+  // of recomputing them (the third of its MFMA work); NULL = recompute
+  float* ucache;
 };
 
 struct GGrads {
@@ -864,6 +871,16 @@ struct GGrads {
 __device__ __forceinline__ float rl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+
+// u cache record of one wave and unit: HB * 16 accumulator values + s + a logit, 64 lanes each
+__device__ __forceinline__ float* ucache_rec(const GArgs& a, int hb_count, int64_t un, int w) {
+  return a.ucache + ((un * GW + w) * int64_t(hb_count * 16 + 2)) * 64;
+}
+size_t ucache_bytes(int H, int64_t b, int64_t n) {
+  const int64_t units = ((b + GW - 1) / GW) * ((n + 31) / 32);
+  return size_t(units * GW * int64_t(((H + 31) / 32) * 16 + 2) * 64) * sizeof(float);
+}
+constexpr size_t UCACHE_MAX_BYTES = size_t(1) << 30;   // above: the backward recomputes u
 
 // The general backward runs one unit per workgroup (persistent = 1 keeps W1 staged across units but
 // spills at D = H = 128: the A/B knob).
@@ -1067,6 +1084,16 @@ gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
       floatx16 acc[HBM];
       float sdot, at;
       gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
+      if (a.ucache) {
+        float* rec = ucache_rec(a, g.HB, un, w) + lane;
+#pragma unroll
+        for (int hb = 0; hb < HBM; ++hb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (hb < g.HB) __builtin_nontemporal_store(acc[hb][r], rec + (hb * 16 + r) * 64);
+        __builtin_nontemporal_store(sdot, rec + (g.HB * 16) * 64);
+        __builtin_nontemporal_store(at, rec + (g.HB * 16 + 1) * 64);
+      }
       float e = 0.f;
       if (n < nj) e = expf(at) * (a.hist[j0 + n] != a.target[c] ? 1.f : 0.f);   // model.py:74-78
       const float S = half_sum(e), N = half_sum(e * sdot);
@@ -1113,7 +1140,17 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     float sdot = 0.f, at = 0.f;
     const int64_t tgt = live ? a.target[c] : -1;
     float e = 0.f;
-    if (live) {
+    if (live && a.ucache) {   // the fused step's forward left u, s and the logit behind
+      const float* rec = ucache_rec(a, g.HB, un, w) + lane;
+#pragma unroll
+      for (int hb = 0; hb < HBM; ++hb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[hb][r] = hb < g.HB ? __builtin_nontemporal_load(rec + (hb * 16 + r) * 64) : 0.f;
+      sdot = __builtin_nontemporal_load(rec + (g.HB * 16) * 64);
+      at = __builtin_nontemporal_load(rec + (g.HB * 16 + 1) * 64);
+      if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
+    } else if (live) {
       gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
       if (n < nj) e = expf(at) * (a.hist[j0 + n] != tgt ? 1.f : 0.f);
     } else {
@@ -1225,7 +1262,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
       }
     }
-    constexpr int OWN = 3;
+    constexpr int OWN = (20 + GW - 1) / GW;   // dW1 tiles per wave: <= 4 hidden x 5 input blocks
     floatx16 gw[OWN];
 #pragma unroll
     for (int q = 0; q < OWN; ++q)
@@ -1488,6 +1525,7 @@ GArgs gargs(const nais_params_t* p, const nais_train_side_t* side, const int64_t
   a.dscale = p->variant == NAIS_VARIANT_DISTANCE ? 1000.f : 100.f;   // model.py:369 / :265
   a.js = g_slice_items(b, n);
   a.drop = make_drop(dropout_p, seed);
+  a.ucache = nullptr;
   return a;
 }
 
@@ -1565,9 +1603,24 @@ int g_backward(const GArgs& a, const float* saved, const float* pred, const floa
 
 extern "C" {
 
+namespace {
+// the fused step's u cache (general kernels only), after saved / gpred / pred / the partials
+size_t step_ucache_bytes(const nais_params_t* params, int64_t b, int64_t n) {
+  if (!params || b <= 0 || n <= 0 || fast_ok(params)) return 0;
+  const size_t u = ucache_bytes(params->hidden, b, n);
+  return u <= UCACHE_MAX_BYTES ? u : 0;
+}
+size_t step_ucache_offset(const nais_params_t* params, int64_t b, int64_t n) {
+  const size_t o = nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);
+  return (o + 255) & ~size_t(255);
+}
+}  // namespace
+
 size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0) return 0;
-  return nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);   // fast or general
+  const size_t u = step_ucache_bytes(params, b, n);   // fast or general (+ the general u cache)
+  return u ? step_ucache_offset(params, b, n) + u
+           : nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);
 }
 
 int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
@@ -1611,6 +1664,9 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
     } else {
       ga = gargs(params, nullptr, hist, n, target, b, dropout_p, seed);
       js = ga.js;
+      if (step_ucache_bytes(params, b, n))
+        ga.ucache = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                             step_ucache_offset(params, b, n));
     }
     ns = (n + js - 1) / js;
     if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
