@@ -963,9 +963,25 @@ struct GL {
 // stage W1 (row-major, pitch Q, zero padded), b1, w2 -- once per (persistent) workgroup
 __device__ __forceinline__ void gm_stage_w(const GArgs& a, const GS& s, const GL& g, float* L, int tid) {
   constexpr int NT = GW * 64;
-  for (int f = tid; f < g.HP32 * g.Q; f += NT) {
-    const int i = f / g.Q, k = f % g.Q;
-    L[g.o_w1 + f] = (i < s.H && k < s.DIN) ? a.w1[int64_t(i) * s.DIN + k] : 0.f;
+  if (s.DIN % 4 == 0 && s.H == g.HP32 && (reinterpret_cast<uintptr_t>(a.w1) & 15) == 0) {
+    // 16-byte global reads (the D = H = 128 shape: 4,096 float4), then the zero pad columns
+    const int R4 = s.DIN / 4;
+    for (int f = tid; f < s.H * R4; f += NT) {
+      const int i = f / R4, k = 4 * (f % R4);
+      const float4 v = reinterpret_cast<const float4*>(a.w1)[f];
+      float* o = L + g.o_w1 + i * g.Q + k;
+      o[0] = v.x;
+      o[1] = v.y;
+      o[2] = v.z;
+      o[3] = v.w;
+    }
+    const int PC = g.Q - s.DIN;
+    for (int f = tid; f < g.HP32 * PC; f += NT) L[g.o_w1 + (f / PC) * g.Q + s.DIN + f % PC] = 0.f;
+  } else {
+    for (int f = tid; f < g.HP32 * g.Q; f += NT) {
+      const int i = f / g.Q, k = f % g.Q;
+      L[g.o_w1 + f] = (i < s.H && k < s.DIN) ? a.w1[int64_t(i) * s.DIN + k] : 0.f;
+    }
   }
   for (int i = tid; i < g.HP32; i += NT) {
     L[g.o_b1 + i] = i < s.H ? a.b1[i] : 0.f;
@@ -1167,7 +1183,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       ds = gl / Sb * e;                                           // dlogit / ds_cj
       da = ds * (sdot - a.beta * N / S);                          // dlogit / da_cj
     }
-    const uint32_t key = (live && a.drop.on) ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
+    const float kscale = a.drop.on ? a.drop.scale : 1.f;
     // du in place; db1 / dw2 as sums over the 32 pairs of each half (reduce-scatter), LDS atomics
   #pragma unroll
     for (int hb = 0; hb < HBM; ++hb) {
@@ -1177,8 +1193,9 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       for (int r = 0; r < 16; ++r) {
         const int i = crow(hb, r, hh);
         const float v = acc[hb][r];
-        const float m = a.drop.on ? a.drop.factor(key, i) : 1.f;
-        const float du = v > 0.f ? da * L[g.o_w2 + i] * m : 0.f;   // ReLU + dropout backward
+        // ReLU + dropout backward: v = u * m > 0 only where the unit was kept (m = scale), so the
+        // mask needs no second hash here -- bit-identical to da * w2 * m
+        const float du = v > 0.f ? da * L[g.o_w2 + i] * kscale : 0.f;
         acc[hb][r] = du;
         vb[r] = du;
         vz[r] = da * nais_relu(v);
