@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, LIB_NAME)
 
 ABI_VERSION = 7
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
+PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
 VARIANT_BASIC, VARIANT_REGION, VARIANT_REGION_DISTANCE, VARIANT_DISTANCE = 0, 1, 2, 3
 FLAG_SIGMOID = 1
@@ -206,7 +207,7 @@ def load(path: str | None = None):
     lib.nais_pair_prior_table.restype = i32
     lib.nais_pair_prior_table.argtypes = [vp, i64, vp, i64, i64, i64, f64, f64, vp, i64, vp]
     lib.nais_pair_prior_gather.restype = i32
-    lib.nais_pair_prior_gather.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, vp, i64, i64, vp, vp]
+    lib.nais_pair_prior_gather.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, vp, i64, i64, vp, i32, vp]
     lib.nais_topk_blend_rows.restype = i32
     lib.nais_topk_blend_rows.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp]
     lib.nais_topk_blend_rows_f64.restype = i32

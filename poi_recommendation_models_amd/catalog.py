@@ -198,6 +198,7 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     if prior is not None:
         pa, pb, alpha, pc = prior
         pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
+        prior_flags = _capi.PRIOR_FINITE if _prior_entries_finite(pa, pb) else 0
         pri = _capi.NaisPrior(float(pa), float(pb), float(alpha), pri_coords.data_ptr())
     nbytes = lib.nais_score_topk_workspace_size(prm, n, k, int(prior is not None))
     ws = _workspace(dev, nbytes)
@@ -412,6 +413,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if prior is not None:
         pa, pb, alpha, pc = prior
         pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
+        prior_flags = _capi.PRIOR_FINITE if _prior_entries_finite(pa, pb) else 0
     pr_of = {}   # column-block table -> its float64 pr_d table (prior only)
     # the L2-blocked gather reads the interleaved table that nais_pair_table_il writes (the NAIS
     # catalog kernels; other cores keep the two row-major tables)
@@ -481,7 +483,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     _capi.check(lib.nais_pair_prior_gather(
                         pr_of[id(tab)].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                         csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, G.data_ptr(), NC, c0_all,
-                        gmax.data_ptr(), stream_), "nais_pair_prior_gather")
+                        gmax.data_ptr(), prior_flags, stream_), "nais_pair_prior_gather")
         if J > 0:
             # two f32 tables (+ the f64 pr_d table with a prior) per buffer, <= budget / 4 each
             W = min(PAIR_BLOCK_COLS, (budget // 4) // ((16 if prior is not None else 8) * J))
@@ -596,6 +598,21 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if return_keys:
         return ids, sc_out, keys_out
     return ids, sc_out
+
+
+def _prior_entries_finite(a, b):
+    """Every pr_d(d) = a * max(0.01, d)^b (powerLaw.py:86-88) is finite for 0 <= d <= half the
+    earth's circumference (the range of powerLaw.dist), so a G product that reached 0.0 stays 0.0
+    (nais_pair_prior_gather's NAIS_PRIOR_FINITE)."""
+    import math
+    a, b = float(a), float(b)
+    if not (math.isfinite(a) and math.isfinite(b)):
+        return False
+    try:
+        ends = (a * 0.01 ** b, a * (math.pi * 6371.0) ** b)
+    except OverflowError:
+        return False
+    return all(math.isfinite(v) for v in ends)
 
 
 def prior_rows(train_matrix, users, a, b, coords, device):

@@ -609,12 +609,16 @@ prior_pair_table_kernel(const double* __restrict__ coords, const int64_t* __rest
 // an empty history, -1.0 for history POIs), and gmax[slot] = max(gmax[slot], max over the block's
 // candidates) as u64 bits (non-negative doubles order as their bits). One wave per user, 4
 // columns per lane, 4 users per workgroup -- the layout of pair_gather_topk_kernel.
+// zero_exit: every pr entry is finite (the caller's (a, b) guarantee it), so a product that has
+// underflowed to 0.0 stays 0.0 (powerLaw.py:92's np.prod does the same): once all of a wave's
+// columns are 0 its remaining rows are not read (long histories underflow: each factor is ~1e-3
+// at city distances, so G reaches 0 after ~110 history POIs). The history bitmap is still built.
 __global__ void __launch_bounds__(GW * 64)
 prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_t* __restrict__ rowmap,
                          const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
                          const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
                          double* __restrict__ G, int64_t g_ld, int64_t g_col0,
-                         unsigned long long* __restrict__ gmax) {
+                         unsigned long long* __restrict__ gmax, int zero_exit) {
   __shared__ uint32_t hm[GW][STRIPE / 32];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t slot = int64_t(blockIdx.x) * GW + w;
@@ -628,7 +632,8 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
   wave_lds_sync();
   double g[CPL];
 #pragma unroll
-  for (int q = 0; q < CPL; ++q) g[q] = 1.0;
+  for (int q = 0; q < CPL; ++q) g[q] = (x + q < cols) ? 1.0 : 0.0;   // columns past the block: 0
+  bool all_zero = false;   // wave-uniform: every column's product is 0.0 (zero_exit only)
   for (int64_t j0 = 0; j0 < hl; j0 += 64) {
     const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
     int64_t mine = 0;
@@ -638,6 +643,7 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
       const int64_t r = c - col0 - s0;
       if (r >= 0 && r < STRIPE && r + s0 < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
     }
+    if (all_zero) continue;   // only the bitmap is left to build
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
     int jj = 0;
     if (full) {   // GU rows' loads in flight (as gather_rows_full), products still in CSR order
@@ -650,13 +656,29 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
         for (int u2 = 0; u2 < GU; ++u2)
 #pragma unroll
           for (int q = 0; q < CPL; ++q) g[q] = __dmul_rn(g[q], rv[u2][q]);
+        if (zero_exit) {
+          bool nz = false;
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) nz |= g[q] != 0.0;
+          if (__ballot(nz) == 0ull) {
+            all_zero = true;
+            break;
+          }
+        }
       }
     }
+    if (all_zero) continue;
     for (; jj < jn; ++jj) {
       const double* row = pr + bcast64(mlo, mhi, jj) + x;
 #pragma unroll
       for (int q = 0; q < CPL; ++q)
         if (x + q < cols) g[q] = __dmul_rn(g[q], row[q]);
+    }
+    if (zero_exit) {
+      bool nz = false;
+#pragma unroll
+      for (int q = 0; q < CPL; ++q) nz |= g[q] != 0.0;
+      all_zero = __ballot(nz) == 0ull;
     }
   }
   wave_lds_sync();
@@ -841,7 +863,7 @@ int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int6
 int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowmap,
                                const int64_t* indptr, const int64_t* indices, const int32_t* users,
                                int32_t num_users, int64_t col0, int64_t cols, double* g, int64_t g_ld,
-                               int64_t g_col0, uint64_t* gmax_bits, void* stream) {
+                               int64_t g_col0, uint64_t* gmax_bits, int32_t flags, void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || col0 < g_col0 || g_ld < col0 - g_col0 + cols)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
   if (num_users == 0 || cols == 0) return NAIS_OK;
@@ -854,7 +876,8 @@ int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowm
                      dim3((unsigned)((num_users + GW - 1) / GW), (unsigned)stripes), dim3(GW * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), pr, ld, rowmap, indptr, indices, users,
                      num_users, col0, cols, g, g_ld, g_col0,
-                     reinterpret_cast<unsigned long long*>(gmax_bits));
+                     reinterpret_cast<unsigned long long*>(gmax_bits),
+                     (flags & NAIS_PRIOR_FINITE) ? 1 : 0);
   return nais_internal_check_launch("prior_pair_gather_kernel");
 }
 

@@ -98,13 +98,16 @@ def test_score_topk_with_prior_blend(strategy):
                                    lookup=dict(zip(cand.tolist(), blended.tolist())))
 
 
-def test_pair_prior_gather_equals_prior_rows_bits():
+@pytest.mark.parametrize("h_max,flags", [(60, 0), (60, 1), (240, 0), (240, 1)])
+def test_pair_prior_gather_equals_prior_rows_bits(h_max, flags):
     """The pairs route's G (nais_pair_prior_table + nais_pair_prior_gather, several column blocks)
-    is bit-identical to nais_powerlaw_prior's rows (the direct route), and so is the per-user max."""
+    is bit-identical to nais_powerlaw_prior's rows (the direct route), and so is the per-user max --
+    also with the underflow exit (flags = NAIS_PRIOR_FINITE) on histories long enough (h up to 240)
+    that whole stripes of G underflow to 0.0 (np.prod's own result, powerLaw.py:92)."""
     from poi_recommendation_models_amd import _capi
     from poi_recommendation_models_amd.catalog import DeviceCSR, prior_rows
     from poi_recommendation_models_amd.synthetic import make_checkins
-    data = make_checkins(40, 1500, 60, seed=8)
+    data = make_checkins(40, 1500, h_max, seed=8)
     P, U = data.num_pois, data.num_users
     a, b = 0.052, -1.37
     dev = torch.device(DEV)
@@ -132,11 +135,13 @@ def test_pair_prior_gather_equals_prior_rows_bits():
                                               pr.data_ptr(), W, st), "nais_pair_prior_table")
         _capi.check(lib.nais_pair_prior_gather(pr.data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                                                csr.indices.data_ptr(), users.data_ptr(), U, c0, w,
-                                               G.data_ptr(), P, 0, gmax.data_ptr(), st),
+                                               G.data_ptr(), P, 0, gmax.data_ptr(), flags, st),
                     "nais_pair_prior_gather")
     torch.cuda.synchronize()
     assert torch.equal(G.view(torch.int64), ref.view(torch.int64))
     assert torch.equal(gmax, ref_max.view(torch.int64))
+    if h_max > 200:   # the case the exit is for: some users' whole rows underflowed
+        assert bool(((G == 0) | (G == -1)).all(dim=1).any())
 
 
 def test_prior_pairs_route_vs_direct_route():
