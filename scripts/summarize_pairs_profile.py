@@ -17,7 +17,7 @@ rows = []
 for sub in ("pmc_fetch", "pmc_write"):
     for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
         n = r["Kernel_Name"]
-        if any(t in n for t in ("pair_gather", "catalog", "topk")):  # noqa: E501
+        if any(t in n for t in ("pair_gather", "catalog", "topk", "gather_rows")):  # noqa: E501
             name = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             rows.append({"kernel": name, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
                          "value_kb": float(r["Counter_Value"]), "grid": r["Grid_Size"],
@@ -33,14 +33,27 @@ with open(os.path.join(dst, "pmc_by_kernel.csv"), "w", newline="") as fh:
     for (kern, ctr), (r0, v) in sorted(agg.items()):
         w.writerow([kern, ctr, len(v), sum(v) / len(v), min(v), max(v), r0["wg"], r0["lds"], r0["vgpr"]])
 out = {}
+# the headline table kernel: basic variant, 8 waves, fp16x6 (3 pieces) -- the fp32 / fp16x3 /
+# region_distance legs' table launches are other instantiations and stay out of the mean
+TABLE = {"fp16x6": "catalog_score_x3b_kernel<32, 2, 0, 8, 3>", "fp16x3": "catalog_score_x3b_kernel<32, 2, 0, 8, 2>"}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
-                 ("catalog", "pairs_table_" + precision)):
+                 (TABLE.get(precision, "catalog"), "pairs_table_" + precision), ("gather_rows", "gather_rows")):
     sel = [r for r in rows if tag in r["kernel"]]
     f = [r["value_kb"] for r in sel if r["counter"] == "FETCH_SIZE"]
     wr = [r["value_kb"] for r in sel if r["counter"] == "WRITE_SIZE"]
     if not f or not wr:
         continue
     fetch, write = sum(f) / len(f), sum(wr) / len(wr)
+    if key == "gather_rows":   # bench.py gather_rows_leg: 4M of 4M rows x d = 128, permutation order
+        out[key] = {"kernel": sel[0]["kernel"], "rows": 4_000_000, "dim": 128, "m": 4_000_000,
+                    "dispatches": len(f), "fetch_size_kb": fetch, "write_size_kb": write,
+                    "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+                    "algorithmic_bytes_per_launch": 4_000_000 * (8 + 8 * 128),
+                    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                              "the bench command (its gather_rows leg); bytes = (2*FETCH_SIZE + "
+                              "WRITE_SIZE)*1024 per launch (MI355X_MICROARCH.md gfx950 correction)",
+                    "source": src}
+        continue
     out[key] = {"kernel": sel[0]["kernel"], "num_users": users, "num_pois": P, "world": world,
                 "block_cols": block_cols, "precision": precision,
                 "dispatches": len(f), "fetch_size_kb": fetch, "write_size_kb": write,
