@@ -265,16 +265,18 @@ _masked: dict = {}
 def auto_table_cus(model, J, NC, entries, ncu, prior=False):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
-    on config 4 and config 5 (profiles/r1/cfg5p/): tables at ~1.1e15 f16 FLOP/s (split-fp16) or
-    1.3e14 FLOP/s (fp32) on the whole chip, scaling with their CUs; gathers at ~60 GB/s per CU up
-    to 7.5 TB/s. Picks the split that minimises the slower of the two streams (config 4: 160 of 256
+    on config 4 and config 5 (profiles/r1/cfg5p/, re-fitted in round 3 on the fp16x6 tables:
+    629-664 ms on 160 CUs): tables at ~1.25e15 f16 FLOP/s (split-fp16) or
+    1.3e14 FLOP/s (fp32) on the whole chip, scaling with their CUs; gathers at ~72 GB/s per CU up
+    to 7.5 TB/s (round 3: measured 71 GB/s per CU at 96 gather CUs, 78 at 64, 59 at 128 where the
+    memory side saturates; the round-1 figure of 60 kept the exact-fp32 leg at 160 table CUs). Picks the split that minimises the slower of the two streams (config 4: 160 of 256
     under fp16x6, config 5: 224). With the power-law prior the table stream also builds the float64
     pr_d table (~1.4e-11 s per pair on the whole chip, profiles/r2/legs_s4) and the gather stream
     reads it too (8 more bytes per history entry and column)."""
     H, din = model.attn_layer1.weight.shape
     prec = getattr(model, "precision", "fp16x6")
     products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
-    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else 1.1e15)
+    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else 1.25e15)
     gbytes = entries * NC * 8.0
     if prior:
         t_tab += J * NC * 1.4e-11
@@ -282,8 +284,8 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False):
     xcd = max(1, ncu // 8)
     best, best_t = ncu // 2, None
     for n in range(ncu // 4, ncu - xcd + 1, xcd):
-        t = max(t_tab * ncu / n, gbytes / min(7.5e12, (ncu - n) * 60e9))
-        if best_t is None or t < best_t:
+        t = max(t_tab * ncu / n, gbytes / min(7.5e12, (ncu - n) * 72e9))
+        if best_t is None or t <= best_t:   # ties (gather-bound): the larger table share
             best, best_t = n, t
     return best
 

@@ -17,6 +17,7 @@ def _model(d, h, precision):
     ("fp16x6", False, 160),   # config 4, the bench default (profiles/r2: 160 / 96 best measured)
     ("fp16x3", False, 128),   # round 1's split
     ("fp16x6", True, 128),    # the prior doubles the gathered bytes
+    ("fp32", False, 192),     # round 3: exact-fp32 tables need the CUs (gather 78 GB/s per CU at 64)
 ])
 def test_config4_splits(precision, prior, want):
     assert auto_table_cus(_model(64, 64, precision), 100_000, 100_000, 5_030_351, 256, prior) == want
