@@ -1448,7 +1448,9 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
           }
         }
       }
+#ifndef NAIS_X3B_DIAG_NOGROUPBAR   // timing-only diagnostic build: the ring then races
       __syncthreads();
+#endif
     }
     if (PIPE && prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
       if (prev & 1)
