@@ -1047,9 +1047,19 @@ struct CfgB {
   // S*b1 and the epilogue is relu + fma (3 VALU per value instead of 4), no VGPRs spent
   static constexpr bool WLDS = NAIS_X3B_WLDS && PIPE && !EREGS;
   static constexpr int ESCL = WLDS ? NW * EPI : 0;
-  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(ADIST) * 4 + size_t(EPI) * 4 +
-                                  size_t(ESCL) * 4 + 64 + size_t(JCB) * D * 4 + size_t(JCB) * 4 +
-                                  (DIST ? size_t(JCB) * 16 : 0);
+  static constexpr size_t REST = size_t(ADIST) * 4 + size_t(EPI) * 4 + size_t(ESCL) * 4 + 64 +
+                                 size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+  // RING1: one ring slot instead of two (fp16x6 at D = H = 128: a 96 KiB item, 2 x 96 KiB do not
+  // fit the 160 KiB LDS) -- build item j, barrier, every wave's MFMAs on it, barrier; the builds
+  // then do not overlap the matrix work, but the A_j build stays once per item and workgroup
+  // (the per-pair split kernel splits x = h (.) t for every pair instead)
+#ifndef NAIS_X3B_RING1
+#define NAIS_X3B_RING1 0   // A/B (round 3): 8.79 vs 8.67 ms per D = H = 128 table block, config-5 direct 6.71e7 vs 6.60e7 pairs/s -- a wash
+#endif
+  static constexpr size_t LDS_MAX = 160 * 1024;
+  static constexpr bool RING1 = NAIS_X3B_RING1 && !PIPE && G == 1 &&
+                                size_t(2) * IB + REST > LDS_MAX && size_t(IB) + REST <= LDS_MAX;
+  static constexpr size_t BYTES = size_t(RING1 ? 1 : 2) * G * IB + REST;
   static_assert(!PIPE || G % 2 == 0, "the pipelined steps alternate two accumulator sets per item");
 };
 
@@ -1074,8 +1084,8 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #endif
   constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][piece][NE]
-  float* Adist = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);
+  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups (1: RING1)][G items][piece][NE]
+  float* Adist = reinterpret_cast<float*>(ring + (C::RING1 ? 1 : 2) * G * NPC * NE);
   float* Eimg = Adist + C::ADIST;
   float* Escl = Eimg + C::EPI;          // WLDS: per wave [S*b1 | w2/S] (EPI floats each)
   float* red = Escl + C::ESCL;
@@ -1417,6 +1427,15 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
       epi.rescale(mine, hh, Sacc, invS);
     } else {
       epi.rescale(Eimg, hh, Sacc, invS);
+    }
+    if constexpr (C::RING1) {   // one slot: build, barrier, consume, barrier
+      for (int jj = 0; jj < jn; ++jj) {
+        if (jj > 0) __syncthreads();   // every wave is done with item jj - 1 (the slot's tenant)
+        build(jj, 0, 0);
+        __syncthreads();
+        step_wide(ring, jj);
+      }
+      continue;   // the next chunk's (or the exit's) barrier orders the last item's reads
     }
     const int ngroups = (jn + G - 1) / G;
 #pragma unroll
