@@ -502,7 +502,17 @@ typedef struct nais_train_side {
   const int64_t* target_region;   /* [b]                                                        */
   const float* target_lat_long;   /* [b, n, 2] f32 (region_distance)                           */
   int64_t latlon_ld;              /* row stride of target_lat_long in elements (>= 2n)         */
+  /* optional u cache (general kernels, nais_train_ucache_size() > 0): with ucache_bytes >= that
+   * size, nais_train_forward_ex leaves every pair's post-dropout W1 x + b1, h . t and attention
+   * logit here and nais_train_backward_ex of the SAME batch, parameters and seed reads them instead
+   * of recomputing the forward (a third of its MFMA work); NULL = recompute */
+  float* ucache;
+  uint64_t ucache_bytes;
 } nais_train_side_t;
+
+/* Bytes of the u cache for (params, b, n): 0 where the fused kernels run (they keep no cache) or
+ * above 1 GiB (the backward then recomputes). */
+size_t nais_train_ucache_size(const nais_params_t* params, int64_t b, int64_t n);
 
 typedef struct nais_train_grads {
   float* embed_history;           /* [P, item_dim]  */
@@ -577,9 +587,10 @@ int32_t nais_make_train_batch(const int64_t* indptr, const int64_t* indices, int
  * torch.optim.Adagrad's update (run.py:89; lr_decay folded into clr = lr / (1 + (step-1) lr_decay)):
  *   g' = g + weight_decay * p ; state += g' * g' ; p -= clr * g' / (sqrt(state) + eps)
  * nais_adagrad: every element of a tensor of numel floats.
- * nais_adagrad_rows: only rows[num_rows] (distinct) of a [*, dim] tensor, weight_decay 0. Rows
- *   whose gradient is zero are left bit-identical by the dense update, so this equals
- *   nais_adagrad when `rows` covers every row with a nonzero gradient.
+ * nais_adagrad_rows: only rows[num_rows] of a [*, dim] tensor, weight_decay 0. Rows whose
+ *   gradient is zero are left bit-identical by the dense update, so this equals nais_adagrad
+ *   when `rows` covers every row with a nonzero gradient. Rows are distinct, or sorted with
+ *   repeats: an entry equal to the one before it is skipped (each row updated once).
  */
 int32_t nais_adagrad(float* param, float* state_sum, const float* grad, int64_t numel, float clr,
                      float weight_decay, float eps, void* stream);

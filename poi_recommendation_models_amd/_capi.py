@@ -32,7 +32,7 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
            "nais_pair_table_il", "nais_pair_gather_topk_l2", "nais_pair_prior_table",
            "nais_pair_prior_gather", "nais_topk_blend_rows", "nais_topk_blend_rows_f64",
-           "nais_topk_merge_f64")
+           "nais_topk_merge_f64", "nais_train_ucache_size")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -45,7 +45,8 @@ class NaisDotTables(ctypes.Structure):
 class NaisTrainSide(ctypes.Structure):
     """Mirror of `nais_train_side_t` (include/nais.h)."""
     _fields_ = [("hist_region", ctypes.c_void_p), ("target_region", ctypes.c_void_p),
-                ("target_lat_long", ctypes.c_void_p), ("latlon_ld", ctypes.c_int64)]
+                ("target_lat_long", ctypes.c_void_p), ("latlon_ld", ctypes.c_int64),
+                ("ucache", ctypes.c_void_p), ("ucache_bytes", ctypes.c_uint64)]
 
 
 class NaisTrainGrads(ctypes.Structure):
@@ -212,6 +213,8 @@ def load(path: str | None = None):
     lib.nais_topk_blend_rows.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp]
     lib.nais_topk_blend_rows_f64.restype = i32
     lib.nais_topk_blend_rows_f64.argtypes = [vp, i64, vp, i64, vp, i64, i32, i32, f64, vp, vp, vp, vp, vp]
+    lib.nais_train_ucache_size.restype = sz
+    lib.nais_train_ucache_size.argtypes = [ctypes.POINTER(NaisParams), i64, i64]
     lib.nais_topk_merge_f64.restype = i32
     lib.nais_topk_merge_f64.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp]
     lib.nais_topk_keys_finish.restype = i32

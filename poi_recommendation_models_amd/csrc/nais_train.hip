@@ -637,9 +637,10 @@ __global__ void adagrad_kernel(float* __restrict__ p, float* __restrict__ st,
   }
 }
 
-// The same update restricted to `rows` of a [*, dim] tensor (rows distinct). With weight_decay 0
-// a row whose gradient is zero is left bit-identical by the dense update (state += 0, p -= 0),
-// so this equals the dense step when `rows` covers every row with a nonzero gradient.
+// The same update restricted to `rows` of a [*, dim] tensor. With weight_decay 0 a row whose
+// gradient is zero is left bit-identical by the dense update (state += 0, p -= 0), so this equals
+// the dense step when `rows` covers every row with a nonzero gradient. An entry equal to the one
+// before it is skipped, so a sorted list with repeats (no device->host sync to dedup) is fine.
 __global__ void adagrad_rows_kernel(float* __restrict__ p, float* __restrict__ st,
                                     const float* __restrict__ g, int dim,
                                     const int64_t* __restrict__ rows, int64_t nrows, float clr,
@@ -647,7 +648,9 @@ __global__ void adagrad_rows_kernel(float* __restrict__ p, float* __restrict__ s
   const int64_t total = nrows * dim;
   for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < total;
        f += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t i = rows[f / dim] * dim + f % dim;
+    const int64_t k = f / dim;
+    if (k > 0 && rows[k] == rows[k - 1]) continue;
+    const int64_t i = rows[k] * dim + f % dim;
     const float gi = g[i];
     const float si = st[i] + gi * gi;
     st[i] = si;
@@ -1632,6 +1635,13 @@ int g_backward(const GArgs& a, const float* saved, const float* pred, const floa
 extern "C" {
 
 namespace {
+// the caller's u cache of the autograd split (nais_train_side_t::ucache), when large enough
+float* side_ucache(const nais_params_t* params, const nais_train_side_t* side, int64_t b, int64_t n) {
+  if (!side || !side->ucache || fast_ok(params) || b <= 0 || n <= 0) return nullptr;
+  const size_t need = ucache_bytes(params->hidden, b, n);
+  return (need <= UCACHE_MAX_BYTES && side->ucache_bytes >= need) ? side->ucache : nullptr;
+}
+
 // the fused step's u cache (general kernels only), after saved / gpred / pred / the partials
 size_t step_ucache_bytes(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0 || n <= 0 || fast_ok(params)) return 0;
@@ -1643,6 +1653,12 @@ size_t step_ucache_offset(const nais_params_t* params, int64_t b, int64_t n) {
   return (o + 255) & ~size_t(255);
 }
 }  // namespace
+
+size_t nais_train_ucache_size(const nais_params_t* params, int64_t b, int64_t n) {
+  if (!params || b <= 0 || n <= 0 || fast_ok(params)) return 0;
+  const size_t u = ucache_bytes(params->hidden, b, n);
+  return u <= UCACHE_MAX_BYTES ? u : 0;
+}
 
 size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, int64_t n) {
   if (!params || b <= 0) return 0;
@@ -1815,7 +1831,8 @@ int32_t nais_train_forward_ex(const nais_params_t* params, const nais_train_side
                        nullptr, nullptr, 0, b, n, params->beta, pred, saved, nan_count);
     return nais_internal_check_launch("train_finalize_kernel");
   }
-  const GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  a.ucache = side_ucache(params, side, b, n);
   const int64_t ns = (n + a.js - 1) / a.js;
   if (ns > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
   if (!workspace || workspace_bytes < g_workspace(b, n))
@@ -1857,7 +1874,8 @@ int32_t nais_train_backward_ex(const nais_params_t* params, const nais_train_sid
     return nais_internal_fail(NAIS_E_INVALID, "distance needs grads->dist_w / dist_b");
   (void)workspace;
   (void)workspace_bytes;
-  const GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  GArgs a = gargs(params, side, hist, n, target, b, dropout_p, seed);
+  a.ucache = side_ucache(params, side, b, n);
   if ((n + a.js - 1) / a.js > 65535) return nais_internal_fail(NAIS_E_UNSUPPORTED, "history too long for the grid");
   const GGrads g{grads->embed_history, grads->embed_target, grads->embed_region, grads->w1,
                  grads->b1, grads->w2, grads->dist_w, grads->dist_b};

@@ -283,7 +283,11 @@ class _NAISTrainStep(torch.autograd.Function):
         b, n = target.shape[0], hist.shape[0]
         lib = _capi.load()
         prm = module.nais_params()
-        sd = _train_side(side)
+        # the general kernels' u cache (D or H beyond the fused kernels' shapes): the forward leaves
+        # each pair's u / s / logit for this Function's backward instead of it recomputing them
+        ub = lib.nais_train_ucache_size(prm, b, n)
+        ucache = torch.empty(ub, dtype=torch.uint8, device=dev) if ub else None
+        sd = _train_side(side, ucache)
         pred = torch.empty(b, dtype=torch.float32, device=dev)
         saved = torch.empty(2 * max(b, 1), dtype=torch.float32, device=dev)
         nan = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -294,7 +298,7 @@ class _NAISTrainStep(torch.autograd.Function):
                                               pred.data_ptr(), saved.data_ptr(), nan.data_ptr(),
                                               ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
                     "nais_train_forward_ex")
-        ctx.module, ctx.p, ctx.seed, ctx.side = module, p, seed, side
+        ctx.module, ctx.p, ctx.seed, ctx.side, ctx.ucache = module, p, seed, side, ucache
         ctx.save_for_backward(hist, target, pred, saved)
         ctx.mark_non_differentiable(nan)
         return pred, nan
@@ -316,7 +320,8 @@ class _NAISTrainStep(torch.autograd.Function):
         prm = m.nais_params()
         ws_bytes = lib.nais_train_workspace_size(prm, b, n)
         ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=dev)
-        _capi.check(lib.nais_train_backward_ex(prm, _train_side(ctx.side), _capi.ptr(hist) if n else None,
+        _capi.check(lib.nais_train_backward_ex(prm, _train_side(ctx.side, ctx.ucache),
+                                               _capi.ptr(hist) if n else None,
                                                n, _capi.ptr(target) if b else None, b, ctx.p, ctx.seed,
                                                pred.data_ptr(), saved.data_ptr(), gpred.data_ptr(),
                                                grads, ws.data_ptr(), ws_bytes, _capi.stream_handle(dev)),
@@ -329,13 +334,15 @@ class _NAISTrainStep(torch.autograd.Function):
         return (None, None, None, None, None, None, *g)
 
 
-def _train_side(side):
+def _train_side(side, ucache=None):
     sd = _capi.NaisTrainSide()
     if side is not None:
         hreg, treg, ll = side
         sd.hist_region, sd.target_region = _capi.ptr(hreg), _capi.ptr(treg)
         if ll is not None:
             sd.target_lat_long, sd.latlon_ld = ll.data_ptr(), ll.stride(0)
+    if ucache is not None:
+        sd.ucache, sd.ucache_bytes = ucache.data_ptr(), ucache.numel()
     return sd
 
 

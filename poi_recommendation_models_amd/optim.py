@@ -68,7 +68,9 @@ class Adagrad(torch.optim.Optimizer):
                 s = st["sum"]
                 stream = _capi.stream_handle(p.device)
                 if isinstance(rows, list) and group["row_update"] and group["weight_decay"] == 0 and p.dim() == 2:
-                    r = torch.unique(torch.cat([x.reshape(-1) for x in rows]))
+                    # sorted with repeats (the kernel skips an entry equal to its predecessor):
+                    # torch.unique would size its output on the host, one sync per table per step
+                    r = torch.sort(torch.cat([x.reshape(-1) for x in rows])).values
                     _capi.check(lib.nais_adagrad_rows(p.data_ptr(), s.data_ptr(), g.data_ptr(),
                                                       p.shape[1], r.data_ptr(), r.numel(), clr,
                                                       group["eps"], stream), "nais_adagrad_rows")

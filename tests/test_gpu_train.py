@@ -212,7 +212,7 @@ def test_adagrad_rows_bit_identical_to_dense():
             g = torch.as_tensor(grads[k]).to(DEV)
             qa.grad, qb.grad = g.clone(), g.clone()
             if i in rows:
-                qa._nais_rows = [rows[i]]
+                qa._nais_rows = [rows[i], rows[i][:7]]     # repeats: each row updated once
         oa.step()
         ob.step()
     for qa, qb, k in zip(pa, pb, NAMES):
@@ -309,7 +309,13 @@ def test_make_batch_negatives_uniform():
 
 @pytest.mark.parametrize("D,H", [(64, 64), (128, 128)])   # fused MFMA kernels / general kernels
 def test_fused_step_matches_dropin(D, H):
-    """NAISTrainer.step == forward + BCELoss + backward + optim.Adagrad (same batch, same dropout)."""
+    """NAISTrainer.step == forward + BCELoss + backward + optim.Adagrad (same batch, same dropout).
+
+    Each step starts both sides from identical parameters and Adagrad sums (copied from the fused
+    side), so summation-order noise of one step cannot compound over the next. Adagrad's update is
+    ill-conditioned where the gradient is ~0 (the first step moves by lr * sign(g)), so elements
+    whose gradient is below 1e-4 of the tensor's largest are left out of the parameter check; the
+    sums (g^2) are checked everywhere."""
     from poi_recommendation_models_amd import optim
     P, n = 3000, 60
     p = _params(P, D, H, 5)
@@ -317,7 +323,12 @@ def test_fused_step_matches_dropin(D, H):
     ma, mb = _model(p, drop_p=0.5), _model(p, drop_p=0.5)
     tr = _trainer(ma, X, lr=0.01)
     ob = optim.Adagrad(mb.parameters(), lr=0.01)
+    names = [k for k, _ in ma.named_parameters()]
     for step in range(3):
+        with torch.no_grad():
+            for (k, a), b in zip(ma.named_parameters(), mb.parameters()):
+                b.copy_(a)
+                ob.state[b]["sum"].copy_(tr.sums[k])
         hist, data, labels = _batch(P, n, 4, seed=step)
         tr.step(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV),
                 torch.as_tensor(labels).to(DEV), dropout_seed=1000 + step)
@@ -329,13 +340,17 @@ def test_fused_step_matches_dropin(D, H):
         finally:
             torch.randint = torch_randint
         mb.loss_func(pred, torch.as_tensor(labels).to(DEV)).backward()
+        grads = {k: (b.grad.detach().cpu().numpy().copy() if b.grad is not None else None)
+                 for k, b in zip(names, mb.parameters())}
         ob.step()
+        for (k, a), b in zip(ma.named_parameters(), mb.parameters()):
+            g = grads[k]
+            live = np.ones(a.shape, bool) if g is None else np.abs(g) > 1e-4 * np.abs(g).max()
+            bad = ~np.isclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
+            assert (bad & live).mean() <= 1e-3, (step, k, int((bad & live).sum()), int(bad.sum()))
+            np.testing.assert_allclose(tr.sums[k].cpu().numpy(), ob.state[b]["sum"].cpu().numpy(),
+                                       rtol=1e-3, atol=1e-9)
     assert tr.finish() > 0
-    for (k, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
-        bad = ~np.isclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
-        assert bad.mean() <= 1e-3, (k, int(bad.sum()))
-        np.testing.assert_allclose(tr.sums[k].cpu().numpy(), ob.state[b]["sum"].cpu().numpy(),
-                                   rtol=1e-3, atol=1e-9)
 
 
 @pytest.mark.parametrize("wd", [0.0, 0.01])
