@@ -13,6 +13,13 @@ OUT = os.path.join(HERE, "libnais_hip.so")
 ARCH = os.environ.get("NAIS_OFFLOAD_ARCH", "gfx950")
 
 
+# nais_kernels.hip: MFMAs in their VGPR form (accumulators in VGPRs, not AGPRs). The one-wave-per-
+# SIMD pair-table kernel (pair_table_x3c_kernel, 256 + AGPRs) otherwise gets AGPR accumulators and
+# pays a v_accvgpr_read per epilogue value; every other kernel of the file compiles identically
+# either way (same VGPR / AGPR counts).
+PER_SRC = {"nais_kernels.hip": ("-mllvm", "-amdgpu-mfma-vgpr-form=1")}
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.sep not in c or os.path.exists(c)):
@@ -37,7 +44,8 @@ def build(force=False, extra=(), out=None):
              "-I", os.path.join(ROOT, "include"), *extra]
     # one object per translation unit, compiled in parallel, then one link
     objs = [OUT_ + "." + os.path.basename(s) + ".o" for s in SRCS]
-    procs = [(subprocess.Popen([hipcc(), *flags, "-c", "-o", o, s], stdout=subprocess.PIPE,
+    procs = [(subprocess.Popen([hipcc(), *flags, *PER_SRC.get(os.path.basename(s), ()), "-c", "-o", o, s],
+                               stdout=subprocess.PIPE,
                                stderr=subprocess.STDOUT, text=True), s) for s, o in zip(SRCS, objs)]
     failed = []
     for pr, s in procs:

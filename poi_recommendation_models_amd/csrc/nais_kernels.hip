@@ -1493,6 +1493,317 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Pair-table kernel "x3c": fp16x6, D = H = 64, NAIS_basic (model.py:57-89 per pair; the headline
+// job's table). The x3b item-side factorisation A_j t_c with ONE wave per SIMD and 64 candidates
+// per wave (two 32-column tiles that share the A_j ring):
+//  * 4 waves x 64 candidates = the same 256 candidates per workgroup, so the A_j build is shared
+//    as in x3b, but each SIMD runs a single instruction stream: the tile-0 MFMA chain of item j
+//    carries the epilogue of tile 1 of item j-1, the tile-1 chain carries tile 0's epilogue of
+//    item j (one accumulator set per tile);
+//  * S*b1 (each chain's first src C) and w2/S live in VGPRs: the epilogue reads no LDS and is two
+//    VALU per value (v_maximum3_f32, a ReLU that keeps NaN as torch.relu does, + fma);
+//  * the next group's A_j is built in slices between the MFMAs instead of as a burst before them;
+//  * the pair's two table entries leave as one store per tile (lane half 0: e, half 1: e*s).
+// Same pieces, products and per-hidden-block accumulation order as x3b; the candidate scale is
+// per wave (64 candidates) instead of per 32, which changes results only where a piece falls into
+// fp16 subnormals (below 2^-37 of the scaled maximum).
+// ---------------------------------------------------------------------------------------------
+// A/B (round 3, profiles/r3/x3c_ab): bit-identical tables to x3b on the config-4 block, 186 pair /
+// fp16x6 / config parity tests green, but 2.41 vs 2.20 ms per 512-column block at J = 100k (-9 %):
+// at one wave per SIMD every LDS-read and barrier wait idles the matrix core, which x3b's second
+// wave per SIMD covers; the lighter instruction stream (2 VALU per epilogue value, half the A_j
+// reads per pair, no epilogue-constant LDS reads in the unpinned form) does not make up for it.
+#ifndef NAIS_X3C
+#define NAIS_X3C 0   // 1 = the fp16x6 D = H = 64 NAIS_basic pair table on x3c instead of x3b
+#endif
+namespace x3c {
+constexpr int NW = 4, TPW = 2, CPB = NW * TPW * 32;   // waves, tiles per wave, candidates per WG
+constexpr int DH = 32, D = 64, HB = 2, KS = 4, NPC = 3;
+constexpr int NE = HB * KS * 64;                       // uint4 fragment entries per item and piece
+constexpr int G = 2, JCB = 32;                         // items per ring group, chunk rows
+constexpr int EPT = NE / (NW * 64);                    // build entries per thread and item (2)
+constexpr int NU = HB * KS;                            // (s, hb) units per tile chain
+constexpr int EPI = 2 * 2 * HB * 16;                   // [b1 | w2][lane half][HB * 16]
+constexpr int SV = NW * TPW * 16 * 64;                 // s tiles in LDS: [wave][tile][reg][lane]
+constexpr size_t BYTES = size_t(2) * G * NPC * NE * 16 + size_t(JCB) * D * 4 + size_t(EPI) * 4 +
+                         64 + size_t(JCB) * 4 + size_t(SV) * 4 + size_t(NW) * EPI * 4;
+static_assert(EPT == TPW, "one build entry per tile phase");
+}  // namespace x3c
+
+__device__ __forceinline__ float relu_keepnan(float v) {
+  return __builtin_elementwise_maximum(v, 0.f);   // v_maximum3_f32: NaN in, NaN out; -0 -> +0
+}
+
+__global__ void __launch_bounds__(x3c::NW * 64, 1)
+pair_table_x3c_kernel(DevParams p, const int64_t* __restrict__ indices, TableOut tab) {
+  using namespace x3c;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);                        // [2][G][NPC][NE]
+  float* hrows = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);   // [JCB][D]
+  float* Eimg = hrows + JCB * D;
+  float* red = Eimg + EPI;
+  int32_t* hid = reinterpret_cast<int32_t*>(red + 16);
+  float* svt = reinterpret_cast<float*>(hid + JCB);                   // [NW][TPW][16][64]
+  float* escl = svt + SV;   // per wave: [S*b1 | w2/S][lane half][HB * 16] (S is wave-uniform)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
+  const int64_t hbeg = (int64_t)blockIdx.y * tab.gi;
+  const int64_t hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  int64_t cand[TPW];
+  bool valid[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    cand[t] = tab.col0 + (int64_t)blockIdx.x * CPB + wave * 64 + t * 32 + (lane & 31);
+    valid[t] = cand[t] < p.P && cand[t] < tab.col0 + tab.cols;
+  }
+
+  // ---- this thread's W1 values for its build entries (fp32; pre-scaled by S_A per chunk)
+  float wv[EPT][8];
+  float wmax = 0.f;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NW * 64;
+    const int ln = e & 63, s = (e >> 6) % KS, hb = (e >> 6) / KS;
+    const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 8 * s;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      wv[q][x] = p.w1[(int64_t)i * p.din + k0 + x];
+      wmax = fmaxf(wmax, fabsf(wv[q][x]));
+    }
+  }
+  for (int f = tid; f < EPI; f += NW * 64) {
+    const int which = f / (2 * HB * 16), rem = f % (2 * HB * 16);
+    const int hh2 = rem / (HB * 16), hr = rem % (HB * 16);
+    const int i = acc_row(hr / 16, hr % 16, hh2);
+    Eimg[f] = which == 0 ? p.b1[i] : p.w2[i];
+  }
+  const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg
+
+  // ---- candidate operands: both tiles scaled by one S_t per wave, split into B fragments
+  half8 tb[TPW][KS][NPC];
+  float St;
+  {
+    float tv[TPW][DH];
+    float tmax = 0.f;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const float* src = p.et + (valid[t] ? cand[t] : p.P - 1) * p.item_dim + hh * DH;
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) {
+        const float4 v = reinterpret_cast<const float4*>(src)[q];
+        tv[t][4 * q] = v.x;
+        tv[t][4 * q + 1] = v.y;
+        tv[t][4 * q + 2] = v.z;
+        tv[t][4 * q + 3] = v.w;
+      }
+#pragma unroll
+      for (int k = 0; k < DH; ++k) tmax = fmaxf(tmax, fabsf(tv[t][k]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+    St = pow2_scale(tmax);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = tv[t][8 * s + e] * St;
+        split_pieces<NPC>(x, tb[t][s]);
+      }
+  }
+
+  floatx16 acc[TPW][HB];
+  const float* bS = escl + wave * EPI + hh * HB * 16;                // S*b1 of this lane's rows
+  const float* wS = escl + wave * EPI + 2 * HB * 16 + hh * HB * 16;  // w2/S of the same rows
+  float SAcur = 1.f;
+  int64_t j0 = 0;
+
+  // build entry q of chunk-local item jj into ring slot dst (all pieces)
+  auto build = [&](int jj, uint4* dst, int q) {
+    const int e = tid + q * NW * 64;
+    const int ln = e & 63, s = (e >> 6) % KS;
+    const float* hr = hrows + jj * D + (ln >> 5) * DH + 8 * s;
+    const float4 h0 = *reinterpret_cast<const float4*>(hr);
+    const float4 h1 = *reinterpret_cast<const float4*>(hr + 4);
+    float a[8];
+    a[0] = wv[q][0] * h0.x;
+    a[1] = wv[q][1] * h0.y;
+    a[2] = wv[q][2] * h0.z;
+    a[3] = wv[q][3] * h0.w;
+    a[4] = wv[q][4] * h1.x;
+    a[5] = wv[q][5] * h1.y;
+    a[6] = wv[q][6] * h1.z;
+    a[7] = wv[q][7] * h1.w;
+    half8 pc[NPC];
+    split_pieces<NPC>(a, pc);
+#pragma unroll
+    for (int q2 = 0; q2 < NPC; ++q2) dst[q2 * NE + e] = *reinterpret_cast<const uint4*>(&pc[q2]);
+  };
+
+  // the pair (chunk item pj, tile t): e and e*s from the attention-logit partial ap
+  auto tail = [&](int t, int pj, float ap) {
+    const float2 aph = lane_halves(ap);
+    const float a = aph.x + aph.y;
+    // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
+    const float sv = svt[((wave * TPW + t) * 16 + (((pj >> 3) << 2) | (pj & 3))) * 64 +
+                         ((pj >> 2) & 1) * 32 + (lane & 31)];
+    const bool keep = hid[pj] != (int32_t)cand[t];
+    const float e = expf(a) * (keep ? 1.f : 0.f);
+    if (valid[t]) {
+      const int64_t o = (hbeg + j0 + pj) * tab.ld + (cand[t] - tab.col0);
+      if (hh == 0) tab_store(tab.e + o, e);
+      else tab_store(tab.es + o, e * sv);
+    }
+  };
+
+  // One phase: tile T's MFMA chain for the item in ring slot src (MMA), the epilogue + tail of
+  // tile 1 - T for chunk item ej (ej >= 0), and (MMA) build entry T of chunk item bj into slot
+  // bdst, in NU units of (6 MFMAs + 4 epilogue values + a build slice)
+  auto phase = [&](auto Tc, auto MMAc, const uint4* src, int ej, int bj, uint4* bdst) {
+    constexpr int T = decltype(Tc)::value, O = 1 - T;
+    constexpr bool MMA = decltype(MMAc)::value;
+    float ap = 0.f;
+    uint4 an[NPC];
+    if constexpr (MMA) {
+#pragma unroll
+      for (int q = 0; q < NPC; ++q) an[q] = src[q * NE + lane];
+    }
+    float4 h0, h1;
+    float a8[8];
+    const int be = tid + T * NW * 64;
+    const int bln = be & 63, bs = (be >> 6) % KS;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int s = u / HB, hb = u % HB;
+      if constexpr (MMA) {
+        half8 a_[NPC];
+#pragma unroll
+        for (int q = 0; q < NPC; ++q) a_[q] = *reinterpret_cast<const half8*>(&an[q]);
+        if (u + 1 < NU) {
+          const int s2 = (u + 1) / HB, hb2 = (u + 1) % HB;
+#pragma unroll
+          for (int q = 0; q < NPC; ++q) an[q] = src[q * NE + (hb2 * KS + s2) * 64 + lane];
+        }
+        if (s == 0) {   // the chain starts at S*b1 (4 broadcast ds_read_b128 per lane half)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[T][hb][r] = bS[hb * 16 + r];
+        }
+        acc[T][hb] = mfma_pieces<NPC>(a_, tb[T][s], acc[T][hb]);
+      }
+#pragma unroll
+      for (int v = u * 4; v < u * 4 + 4; ++v)
+        ap = __builtin_fmaf(wS[v], relu_keepnan(acc[O][v / 16][v % 16]), ap);
+      asm volatile("" : "+v"(ap));   // keep the slice in this unit (else it sinks to the tail)
+      if constexpr (MMA) {   // every item step builds; a slot built for a row past jn is never read
+        if (u == 1) {
+          const float* hr = hrows + bj * D + (bln >> 5) * DH + 8 * bs;
+          h0 = *reinterpret_cast<const float4*>(hr);
+          h1 = *reinterpret_cast<const float4*>(hr + 4);
+        } else if (u == 2) {
+          a8[0] = wv[T][0] * h0.x;
+          a8[1] = wv[T][1] * h0.y;
+          a8[2] = wv[T][2] * h0.z;
+          a8[3] = wv[T][3] * h0.w;
+          a8[4] = wv[T][4] * h1.x;
+          a8[5] = wv[T][5] * h1.y;
+          a8[6] = wv[T][6] * h1.z;
+          a8[7] = wv[T][7] * h1.w;
+        } else if (u == 4) {
+          half8 pc[NPC];
+          split_pieces<NPC>(a8, pc);
+#pragma unroll
+          for (int q2 = 0; q2 < NPC; ++q2) bdst[q2 * NE + be] = *reinterpret_cast<const uint4*>(&pc[q2]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ej >= 0) tail(O, ej, ap);
+  };
+
+  for (j0 = 0; j0 < hlen; j0 += JCB) {
+    const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
+    __syncthreads();   // the previous chunk's ring, hrows and hid readers are done
+    float hmax = 0.f;
+    for (int f = tid; f < jn * (D / 4); f += NW * 64) {
+      const int jj = f / (D / 4), q4 = f % (D / 4);
+      const int64_t item = indices[hbeg + j0 + jj];
+      const float4 v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
+      reinterpret_cast<float4*>(hrows)[f] = v;
+      hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int jj = tid; jj < jn; jj += NW * 64) hid[jj] = (int32_t)indices[hbeg + j0 + jj];
+    const float Hm = block_max_n<NW>(hmax, red);   // barrier: chunk published
+    const float SA = pow2_scale(Wmax * Hm);
+    const float rs = SA / SAcur;                   // exact power-of-two ratio
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) wv[q][x] *= rs;
+    SAcur = SA;
+    const float Sacc = SA * St, invS = 1.f / Sacc;
+    for (int f = lane; f < EPI; f += 64)   // this wave's S*b1 and w2/S (published by the barrier below)
+      escl[wave * EPI + f] = Eimg[f] * (f < 2 * HB * 16 ? Sacc : invS);
+    {   // s tiles: rows = the chunk's items (pieces of h * S_h), columns = the tiles' candidates;
+        // kept in LDS (this wave's own region) as s = tile value / (S_h S_t)
+      const float Sh = pow2_scale(Hm);
+      const float invShSt = 1.f / (Sh * St);
+      const int m = lane & 31;
+      floatx16 sacc[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[t][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        float x[8];
+        const float* hp = hrows + m * D + hh * DH + 8 * s;
+        const float4 h0 = *reinterpret_cast<const float4*>(hp);
+        const float4 h1 = *reinterpret_cast<const float4*>(hp + 4);
+        const bool ok = m < jn;
+        x[0] = ok ? h0.x * Sh : 0.f; x[1] = ok ? h0.y * Sh : 0.f;
+        x[2] = ok ? h0.z * Sh : 0.f; x[3] = ok ? h0.w * Sh : 0.f;
+        x[4] = ok ? h1.x * Sh : 0.f; x[5] = ok ? h1.y * Sh : 0.f;
+        x[6] = ok ? h1.z * Sh : 0.f; x[7] = ok ? h1.w * Sh : 0.f;
+        half8 hpc[NPC];
+        split_pieces<NPC>(x, hpc);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) sacc[t] = mfma_pieces<NPC>(hpc, tb[t][s], sacc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) svt[((wave * TPW + t) * 16 + r) * 64 + lane] = sacc[t][r] * invShSt;
+    }
+    const int ngroups = (jn + G - 1) / G;
+#pragma unroll
+    for (int it = 0; it < G; ++it)
+      if (it < jn)
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) build(it, ring + (it * NPC) * NE, q);
+    __syncthreads();
+    int prev = -1;   // chunk-local item whose tile-1 epilogue is pending in acc[1]
+    for (int g = 0; g < ngroups; ++g) {
+#pragma unroll
+      for (int it = 0; it < G; ++it) {
+        const int jj = g * G + it;
+        if (jj < jn) {
+          const uint4* src = ring + (((g & 1) * G + it) * NPC) * NE;
+          const int bj = ((g + 1) * G + it) & (JCB - 1);   // rows past jn: stale, never read
+          uint4* bdst = ring + ((((g + 1) & 1) * G + it) * NPC) * NE;
+          phase(std::integral_constant<int, 0>{}, std::true_type{}, src, prev, bj, bdst);
+          phase(std::integral_constant<int, 1>{}, std::true_type{}, src, jj, bj, bdst);
+          prev = jj;
+        }
+      }
+      __syncthreads();
+    }
+    if (prev >= 0)   // drain: tile 1's epilogue of the chunk's last item, no MFMAs
+      phase(std::integral_constant<int, 0>{}, std::false_type{}, ring, prev, 0, ring);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Top-k per user (validation.py:26-27): exact radix select on 64-bit keys
 //   key = ordered(score) << 32 | (0xFFFFFFFF - poi)   -> unique; larger key = (higher score, lower id)
 // MSB-first 8-bit passes over the user's score row until the keys at or above the selected prefix
@@ -2450,7 +2761,19 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
     tab.es = cs ? nullptr : es + base * ld;
     tab.col0 = col0;
     const int ng = (int)((tab.nitems + tab.gi - 1) / tab.gi);
-    if (params->precision == NAIS_PRECISION_FP32)
+    if (NAIS_X3C && params->precision == NAIS_PRECISION_FP16X6 &&
+        params->variant == NAIS_VARIANT_BASIC && params->embed_dim == 64 && params->hidden == 64 &&
+        cs == 0) {
+      static bool attr_set = false;
+      if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pair_table_x3c_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3c::BYTES);
+        attr_set = true;
+      }
+      hipLaunchKernelGGL(pair_table_x3c_kernel, table_grid(tab, ng, x3c::CPB), dim3(x3c::NW * 64),
+                         x3c::BYTES, st, d, items + base, tab);
+      rc = check_launch("pair_table_x3c_kernel");
+    } else if (params->precision == NAIS_PRECISION_FP32)
       NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, nullptr, items + base, nullptr,
                     ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
     else if (params->precision == NAIS_PRECISION_FP16X6 ||

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lib", action="append", default=[])
     ap.add_argument("--only", default="fp16x6")
+    ap.add_argument("--layout", default="rows", choices=["rows", "il"],
+                    help="rows: nais_pair_table (two row-major tables, the bench's layout); "
+                         "il: nais_pair_table_il (interleaved chunk-major)")
     a = ap.parse_args()
     from poi_recommendation_models_amd import _capi
     from poi_recommendation_models_amd.model import NAIS_basic
@@ -43,7 +46,10 @@ def main():
         name, path = spec.split("=", 1)
         libs[name] = _capi.load(path)
     variants = [(ln, prec) for ln in libs for prec in a.only.split(",")]
-    tabs = {v: torch.empty((W + 63) // 64, J, 128, device=dev) for v in variants}
+    if a.layout == "il":
+        tabs = {v: torch.empty((W + 63) // 64, J, 128, device=dev) for v in variants}
+    else:   # e rows then e*s rows, ld = W
+        tabs = {v: torch.empty(2, J, W, device=dev) for v in variants}
     st = torch.cuda.current_stream(dev)
     times = {v: [] for v in variants}
     for r in range(a.rounds + 1):
@@ -55,9 +61,14 @@ def main():
             e0.record(st)
             for b in range(a.blocks):
                 c0 = (b * W) % (P - W)
-                _capi.check(lib.nais_pair_table_il(prm, items.data_ptr(), J, c0, W, None, None, None,
-                                                   tabs[v].data_ptr(), J * 128, st.cuda_stream),
-                            "nais_pair_table_il")
+                if a.layout == "il":
+                    _capi.check(lib.nais_pair_table_il(prm, items.data_ptr(), J, c0, W, None, None, None,
+                                                       tabs[v].data_ptr(), J * 128, st.cuda_stream),
+                                "nais_pair_table_il")
+                else:
+                    _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, W, None, None, None,
+                                                    tabs[v][0].data_ptr(), tabs[v][1].data_ptr(), W,
+                                                    st.cuda_stream), "nais_pair_table")
             e1.record(st)
             torch.cuda.synchronize(dev)
             if r > 0:
@@ -68,6 +79,8 @@ def main():
     for v in variants:
         ms = float(np.median(times[v]))
         d = float((tabs[v] - base).abs().max().item())
+        rel = float(((tabs[v] - base).abs() / base.abs().clamp_min(1e-30)).max().item())
+        out.setdefault("max_rel_diff_vs_first", {})["%s/%s" % v] = rel
         out["%s/%s" % v] = {"ms_per_block": ms, "tflops": flop / ms / 1e9, "max_abs_diff_vs_first": d}
         print("%-24s %8.3f ms/block  %6.1f TF/s  max|d| %.3g" % ("%s/%s" % v, ms, flop / ms / 1e9, d),
               flush=True)
