@@ -698,12 +698,21 @@ struct Consts16 {
   static constexpr size_t BYTES = size_t(A16) * 16 + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64;
 };
 
-// ReLU on the float bits that keeps every NaN, as torch.relu (model.py:71): as int32, negative
+#ifndef NAIS_RELU_MAXIMUM3
+#define NAIS_RELU_MAXIMUM3 1
+#endif
+// ReLU that keeps every NaN, as torch.relu (model.py:71). Default: gfx950's v_maximum3_f32 (IEEE
+// 754-2019 maximum: NaN propagates, max(-0, +0) = +0), one VALU. A/B (NAIS_RELU_MAXIMUM3=0): on the
+// float bits, as int32, negative
 // non-NaN floats (-0 .. -inf) are <= 0xFF800000 = -8388608 -> 0.0f; positive values (>= 0) and
 // NaNs of either sign (0xFF800001..0xFFFFFFFF = -8388607..-1) pass unchanged. v_cmp + v_cndmask;
 // a v_max_i32 alone would zero a NaN whose sign bit is set.
 __device__ __forceinline__ float relu_bits(float v) {
+#if NAIS_RELU_MAXIMUM3
+  return __builtin_elementwise_maximum(v, 0.f);   // v_maximum3_f32: IEEE maximum, NaN in -> NaN out
+#else
   return (__float_as_int(v) >= -8388607) ? v : 0.f;
+#endif
 }
 
 template <int HB, bool REGS>
