@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -875,9 +876,12 @@ __device__ __forceinline__ float rl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-// u cache record of one wave and unit: HB * 16 accumulator values + s + a logit, 64 lanes each
-__device__ __forceinline__ float* ucache_rec(const GArgs& a, int hb_count, int64_t un, int w) {
-  return a.ucache + ((un * GW + w) * int64_t(hb_count * 16 + 2)) * 64;
+// u cache record of one (slice, batch row): HB * 16 accumulator values + s + a logit, 64 lanes
+// each, in the forward's order (unit un = slice * row tiles + tile, wave w: sl * tiles * GW + c),
+// so a backward with another rows-per-workgroup split finds the same records
+__device__ __forceinline__ float* ucache_rec(const GArgs& a, int hb_count, int64_t sl, int64_t c) {
+  const int64_t nrt = (a.b + GW - 1) / GW;
+  return a.ucache + ((sl * nrt * GW + c) * int64_t(hb_count * 16 + 2)) * 64;
 }
 size_t ucache_bytes(int H, int64_t b, int64_t n) {
   const int64_t units = ((b + GW - 1) / GW) * ((n + 31) / 32);
@@ -945,7 +949,7 @@ struct GL {
   int DBX, XP, UP;              // x blocks of the dW1 tiles (ceil(DIN/32)), stage pitches
   int o_w1, o_b1, o_w2, o_hs, o_ts, o_fs, fwd;
   int o_gh, o_su, o_sx, o_gb, o_gw, o_gd, bwd;
-  __host__ __device__ GL(int D, int H, int DIN) {
+  __host__ __device__ GL(int D, int H, int DIN, int gw = GW) {
     HB = (H + 31) / 32;
     HP32 = HB * 32;
     DINP = (DIN + 1) & ~1;
@@ -959,8 +963,8 @@ struct GL {
     o_w2 = o_b1 + HP32;
     o_hs = o_w2 + HP32;                 // [32][HD] full history rows of the slice
     o_ts = o_hs + 32 * HD;              // [GW][D]  full target rows of the workgroup
-    o_fs = o_ts + GW * D;               // [GW][32][4] f0, f1, 100 lat, 100 lng (region_distance)
-    fwd = o_fs + GW * 32 * 4;
+    o_fs = o_ts + gw * D;               // [GW][32][4] f0, f1, 100 lat, 100 lng (region_distance)
+    fwd = o_fs + gw * 32 * 4;
     o_gh = fwd;                         // [32][HD] history-row grads of the slice (odd pitch:
                                         //          the 32 lanes' items hit distinct banks)
     o_su = o_gh + 32 * HD;              // [2][32][UP] du^T stages (one wave's pairs each; double
@@ -975,8 +979,9 @@ struct GL {
 };
 
 // stage W1 (row-major, pitch Q, zero padded), b1, w2 -- once per (persistent) workgroup
+template <int GWT = GW>
 __device__ __forceinline__ void gm_stage_w(const GArgs& a, const GS& s, const GL& g, float* L, int tid) {
-  constexpr int NT = GW * 64;
+  constexpr int NT = GWT * 64;
   if (s.DIN % 4 == 0 && s.H == g.HP32 && (reinterpret_cast<uintptr_t>(a.w1) & 15) == 0) {
     // 16-byte global reads (the D = H = 128 shape: 4,096 float4), then the zero pad columns
     const int R4 = s.DIN / 4;
@@ -1004,20 +1009,21 @@ __device__ __forceinline__ void gm_stage_w(const GArgs& a, const GS& s, const GL
 }
 
 // one work unit's operands: the slice's full history rows, the row tile's full target rows
+template <int GWT = GW>
 __device__ __forceinline__ void gm_stage(const GArgs& a, const GS& s, const GL& g, float* L, int tid,
                                          int64_t c0, int64_t j0, int nj) {
-  constexpr int NT = GW * 64;
+  constexpr int NT = GWT * 64;
   for (int f = tid; f < 32 * g.HD; f += NT) {
     const int n = f / g.HD, d = f % g.HD;
     L[g.o_hs + f] = (n < nj && d < s.D) ? hfull(a, j0 + n, d) : 0.f;
   }
-  for (int f = tid; f < GW * s.D; f += NT) {
+  for (int f = tid; f < GWT * s.D; f += NT) {
     const int w = f / s.D, d = f % s.D;
     const int64_t c = c0 + w;
     L[g.o_ts + f] = c < a.b ? tfull(a, c, d) : 0.f;
   }
   if (s.DIN > s.D) {
-    for (int f = tid; f < GW * 32; f += NT) {
+    for (int f = tid; f < GWT * 32; f += NT) {
       const int w = f / 32, n = f % 32;
       const int64_t c = c0 + w;
       float f0 = 0.f, f1 = 0.f, l0 = 0.f, l1 = 0.f;
@@ -1090,32 +1096,34 @@ __device__ __forceinline__ float half_sum(float v) {
   return v;
 }
 
-template <int HBM, int DC = 0, int HC = 0, int XC = 0>
-__global__ void __launch_bounds__(GW * 64)
-gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
+// GWT rows (waves) per workgroup, slices sl0, sl0 + 1, ... (g_forward's split launch, as the
+// backward's)
+template <int HBM, int DC = 0, int HC = 0, int XC = 0, int GWT = GW>
+__global__ void __launch_bounds__(GWT * 64)
+gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np, int32_t sl0) {
   extern __shared__ float4 glds4[];
   float* Lb = reinterpret_cast<float*>(glds4);
   const GS s = make_gs<DC, HC, XC>(a);
-  const GL g(s.D, s.H, s.DIN);
+  const GL g(s.D, s.H, s.DIN, GWT);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
-  // persistent: W1 staged once, then work units (row tile of GW rows, slice of 32 items), row
+  // persistent: W1 staged once, then work units (row tile of GWT rows, slice of 32 items), row
   // tile fastest, strided over the grid
-  gm_stage_w(a, s, g, Lb, tid);
-  const int64_t nrt = (a.b + GW - 1) / GW, units = nrt * ((a.n + 31) / 32);
+  gm_stage_w<GWT>(a, s, g, Lb, tid);
+  const int64_t nrt = (a.b + GWT - 1) / GWT, units = nrt * ((a.n + 31) / 32 - sl0);
   for (int64_t un = blockIdx.x; un < units; un += gridDim.x) {
-    const int64_t sl = un / nrt, c0 = (un % nrt) * GW, c = c0 + w;
+    const int64_t sl = sl0 + un / nrt, c0 = (un % nrt) * GWT, c = c0 + w;
     const int64_t j0 = sl * 32;
     const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
     __syncthreads();   // the previous unit's operand reads are done
     float* L = opaque_lds(Lb);
-    gm_stage(a, s, g, L, tid, c0, j0, nj);
+    gm_stage<GWT>(a, s, g, L, tid, c0, j0, nj);
     __syncthreads();
     if (c < a.b) {
       floatx16 acc[HBM];
       float sdot, at;
       gm_pair_forward<HBM>(a, s, g, L, w, lane, c, j0, acc, sdot, at);
       if (a.ucache) {
-        float* rec = ucache_rec(a, g.HB, un, w) + lane;
+        float* rec = ucache_rec(a, g.HB, sl, c) + lane;
 #pragma unroll
         for (int hb = 0; hb < HBM; ++hb)
 #pragma unroll
@@ -1135,34 +1143,37 @@ gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np) {
   }
 }
 
-template <int HBM, int DC = 0, int HC = 0, int XC = 0>
-__global__ void __launch_bounds__(GW * 64, 1)
+// GWT rows (waves) per workgroup; the units cover slices sl0, sl0 + 1, ... (g_backward's split
+// launch: GW rows over the full 32-item slices, GW_TAIL rows over a short last slice)
+template <int HBM, int DC = 0, int HC = 0, int XC = 0, int GWT = GW>
+__global__ void __launch_bounds__(GWT * 64, 1)
 gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
-                   const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows) {
+                   const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows,
+                   int32_t sl0) {
   if (bad_rows && *bad_rows) return;   // fused step on a NaN batch: no update (see train_loss)
   extern __shared__ float4 glds4[];
   float* Lb = reinterpret_cast<float*>(glds4);
   const GS s = make_gs<DC, HC, XC>(a);
-  const GL g(s.D, s.H, s.DIN);
+  const GL g(s.D, s.H, s.DIN, GWT);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31, hh = lane >> 5;
   // persistent: W1 staged once and db1 / dw2 / dist_layer grads kept in LDS across all of the
-  // workgroup's units (row tile of GW rows, slice of 32 items), flushed once; the dW1 tiles and the
+  // workgroup's units (row tile of GWT rows, slice of 32 items), flushed once; the dW1 tiles and the
   // history-row grads are flushed per unit (registers: the dW1 tiles are live in its last phase only)
-  gm_stage_w(a, s, g, Lb, tid);
-  for (int f = tid; f < 2 * g.HP32 + 8; f += GW * 64) Lb[g.o_gb + f] = 0.f;
+  gm_stage_w<GWT>(a, s, g, Lb, tid);
+  for (int f = tid; f < 2 * g.HP32 + 8; f += GWT * 64) Lb[g.o_gb + f] = 0.f;
   const int ntile = g.HB * g.DBX;
-  const int64_t nrt = (a.b + GW - 1) / GW, units = nrt * ((a.n + 31) / 32);
+  const int64_t nrt = (a.b + GWT - 1) / GWT, units = nrt * ((a.n + 31) / 32 - sl0);
   // one unit: the loop body of the persistent form (a lambda, so that the one-unit-per-workgroup
   // launch below carries no loop state -- the persistent loop spills the D = H = 128 backward)
   auto unit = [&](int64_t un) {
-    const int64_t sl = un / nrt, c0 = (un % nrt) * GW, c = c0 + w;
+    const int64_t sl = sl0 + un / nrt, c0 = (un % nrt) * GWT, c = c0 + w;
     const bool live = c < a.b;
     const int64_t j0 = sl * 32;
     const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
     __syncthreads();   // the previous unit's operand reads and grad flush are done
     float* L = opaque_lds(Lb);
-    gm_stage(a, s, g, L, tid, c0, j0, nj);
-    for (int f = tid; f < 32 * g.HD; f += GW * 64) L[g.o_gh + f] = 0.f;
+    gm_stage<GWT>(a, s, g, L, tid, c0, j0, nj);
+    for (int f = tid; f < 32 * g.HD; f += GWT * 64) L[g.o_gh + f] = 0.f;
     __syncthreads();
 
     // ---- recompute the forward, then du in place (C layout)
@@ -1171,7 +1182,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     const int64_t tgt = live ? a.target[c] : -1;
     float e = 0.f;
     if (live && a.ucache) {   // the fused step's forward left u, s and the logit behind
-      const float* rec = ucache_rec(a, g.HB, un, w) + lane;
+      const float* rec = ucache_rec(a, g.HB, sl, c) + lane;
 #pragma unroll
       for (int hb = 0; hb < HBM; ++hb)
 #pragma unroll
@@ -1293,7 +1304,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
       }
     }
-    constexpr int OWN = (20 + GW - 1) / GW;   // dW1 tiles per wave: <= 4 hidden x 5 input blocks
+    constexpr int OWN = (20 + GWT - 1) / GWT;   // dW1 tiles per wave: <= 4 hidden x 5 input blocks
     floatx16 gw[OWN];
 #pragma unroll
     for (int q = 0; q < OWN; ++q)
@@ -1302,7 +1313,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     // ---- dW1 = sum over the workgroup's pairs of du x^T: each wave's 32 pairs of du staged in
     // turn (double-buffered: wave rd + 1 stages while every wave consumes wave rd's), x recomputed
     // from the LDS rows by the consumers; every wave accumulates the output tiles it owns (tiles w,
-    // w + GW, w + 2 GW). One barrier per round.
+    // w + GWT, w + 2 GWT). One barrier per round.
     const int ntile = g.HB * g.DBX;
     auto stage_du = [&](int buf) {
       float* dst = L + (buf ? g.o_sx : g.o_su) + n * g.UP;
@@ -1314,12 +1325,12 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     };
     if (w == 0) stage_du(0);
     __syncthreads();
-    for (int rd = 0; rd < GW; ++rd) {
-      if (rd + 1 < GW && w == rd + 1) stage_du((rd + 1) & 1);
+    for (int rd = 0; rd < GWT; ++rd) {
+      if (rd + 1 < GWT && w == rd + 1) stage_du((rd + 1) & 1);
       const float* su = L + ((rd & 1) ? g.o_sx : g.o_su);
   #pragma unroll
       for (int q = 0; q < OWN; ++q) {
-        const int tile = w + q * GW;
+        const int tile = w + q * GWT;
         if (tile >= ntile) continue;
         const int ib = tile / g.DBX, xb = tile % g.DBX;
   #pragma unroll 4
@@ -1333,7 +1344,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     // ---- the unit's dW1 tiles
   #pragma unroll
     for (int q = 0; q < OWN; ++q) {
-      const int tile = w + q * GW;
+      const int tile = w + q * GWT;
       if (tile >= ntile) continue;
       const int ib = tile / g.DBX, xb = tile % g.DBX;
   #pragma unroll
@@ -1343,7 +1354,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       }
     }
     // ---- the unit's history-row grads (the last dW1 round's barrier ordered every LDS atomic)
-    for (int f = tid; f < nj * s.D; f += GW * 64) {
+    for (int f = tid; f < nj * s.D; f += GWT * 64) {
       const int jj = f / s.D, d = f % s.D;
       const int64_t j = j0 + jj;
       const float v = L[g.o_gh + jj * g.HD + d];
@@ -1358,15 +1369,15 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   }
   // ---- flush (once per workgroup): db1 / dw2, dist_layer
   __syncthreads();
-  for (int i = tid; i < s.H; i += GW * 64) {
+  for (int i = tid; i < s.H; i += GWT * 64) {
     unsafeAtomicAdd(&gr.b1[i], Lb[g.o_gb + i]);
     unsafeAtomicAdd(&gr.w2[i], Lb[g.o_gw + i]);
   }
   if (s.DIN > s.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], Lb[g.o_gd + tid]);
 }
 
-size_t g_lds_bytes(const GArgs& a, bool backward) {
-  const GL g(a.D, a.H, a.DIN);
+size_t g_lds_bytes(const GArgs& a, bool backward, int gw = GW) {
+  const GL g(a.D, a.H, a.DIN, gw);
   return size_t(backward ? g.bwd : g.fwd) * sizeof(float);
 }
 
@@ -1583,51 +1594,94 @@ int device_cus() {
 // the backward at D = 128 with the 2 distance inputs spills (256 VGPRs + 36): runtime-shaped there
 #define NAIS_GM_SHAPES_BWD(X) X(4, 128, 128, 0) X(2, 64, 64, 0) X(2, 64, 64, 2)
 
-int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
-  const size_t lds = g_lds_bytes(a, false);
-#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_forward_kernel<HBM, DC, HC, XC>, 160 * 1024),
-  static bool once = (NAIS_GM_SHAPES(NAIS_GM_LDS) set_lds(gm_forward_kernel<4>, 160 * 1024),
-                      set_lds(gm_forward_kernel<2>, 160 * 1024), true);
+template <int GWT>
+int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64_t units, int sl0) {
+  const size_t lds = g_lds_bytes(a, false, GWT);
+#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_forward_kernel<HBM, DC, HC, XC, GWT>, 160 * 1024),
+  static bool once = (NAIS_GM_SHAPES(NAIS_GM_LDS) set_lds(gm_forward_kernel<4, 0, 0, 0, GWT>, 160 * 1024),
+                      set_lds(gm_forward_kernel<2, 0, 0, 0, GWT>, 160 * 1024), true);
 #undef NAIS_GM_LDS
   (void)once;
   // persistent: one workgroup per CU (the LDS image holds one), units strided over the grid
-  const int64_t units = ((a.b + GW - 1) / GW) * ((a.n + 31) / 32);
   dim3 grid((unsigned)std::min<int64_t>(units, device_cus()));
 #define NAIS_GM_FWD(HBM, DC, HC, XC)                                                        \
   if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
-    hipLaunchKernelGGL((gm_forward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, Sp, Np); \
+    hipLaunchKernelGGL((gm_forward_kernel<HBM, DC, HC, XC, GWT>), grid, dim3(GWT * 64), lds, st, a, \
+                       Sp, Np, sl0);                                                       \
     return nais_internal_check_launch("gm_forward_kernel");                                \
   }
   NAIS_GM_SHAPES(NAIS_GM_FWD)
 #undef NAIS_GM_FWD
-  if (a.H > 64) hipLaunchKernelGGL(gm_forward_kernel<4>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
-  else hipLaunchKernelGGL(gm_forward_kernel<2>, grid, dim3(GW * 64), lds, st, a, Sp, Np);
+  if (a.H > 64)
+    hipLaunchKernelGGL((gm_forward_kernel<4, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0);
+  else
+    hipLaunchKernelGGL((gm_forward_kernel<2, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0);
   return nais_internal_check_launch("gm_forward_kernel");
 }
 
-int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
-               const GGrads& g, hipStream_t st, const int32_t* bad_rows = nullptr) {
-  const size_t lds = g_lds_bytes(a, true);
-#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_backward_kernel<HBM, DC, HC, XC>, 160 * 1024),
-  static bool once = (NAIS_GM_SHAPES_BWD(NAIS_GM_LDS) set_lds(gm_backward_kernel<4>, 160 * 1024),
-                      set_lds(gm_backward_kernel<2>, 160 * 1024), true);
+#ifndef NAIS_GM_TAIL
+#define NAIS_GM_TAIL 4   // rows per workgroup of the short-slice launches; 0 = one launch each
+#endif
+// The general kernels' units are (row tile, 32-item slice) workgroups, one per CU (LDS). When the
+// short last slice (n % 32 items) pushes the unit count into one more round of workgroups over the
+// CUs -- config 3: 85 row tiles x 7 slices = 595 units = 2.3 rounds of 256, the third almost empty
+// but as long as a full one, since a slice of 12 items costs the MFMAs of 32 -- that slice runs as
+// a second launch of NAIS_GM_TAIL-row workgroups (one wave per SIMD, a third of a unit's waves)
+// after the full slices' exactly-filled rounds (the backward; see g_forward). Returns the number of
+// full slices to launch first (== the slice count when no split pays).
+int64_t g_split_slices(const GArgs& a) {
+  const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32, nfull = a.n / 32;
+  const int64_t cus = device_cus();
+  if (NAIS_GM_TAIL <= 0 || nfull == 0 || nsl == nfull) return nsl;
+  const char* off = getenv("NAIS_GM_TAIL");   // "0": one launch (tests compare both forms)
+  if (off && off[0] == '0' && off[1] == 0) return nsl;
+  const int64_t rounds_all = (nrt * nsl + cus - 1) / cus, rounds_full = (nrt * nfull + cus - 1) / cus;
+  return rounds_full < rounds_all ? nfull : nsl;
+}
+
+// The forward stays one persistent launch: its workgroups stage W1 once for all their units, so
+// the short slice's units ride on workgroups that already hold it (A/B, config 3 at D = H = 128:
+// split 0.129 ms vs 0.110 ms -- a 4-row tail workgroup pays a whole W1 staging for one unit).
+int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
+  const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
+  return g_forward_launch<GW>(a, Sp, Np, st, nrt * nsl, 0);
+}
+
+template <int GWT>
+int g_backward_launch(const GArgs& a, const float* saved, const float* pred, const float* gpred,
+                      const GGrads& g, hipStream_t st, const int32_t* bad_rows, int64_t units, int sl0) {
+  const size_t lds = g_lds_bytes(a, true, GWT);
+#define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_backward_kernel<HBM, DC, HC, XC, GWT>, 160 * 1024),
+  static bool once = (NAIS_GM_SHAPES_BWD(NAIS_GM_LDS) set_lds(gm_backward_kernel<4, 0, 0, 0, GWT>, 160 * 1024),
+                      set_lds(gm_backward_kernel<2, 0, 0, 0, GWT>, 160 * 1024), true);
 #undef NAIS_GM_LDS
   (void)once;
-  const int64_t units = ((a.b + GW - 1) / GW) * ((a.n + 31) / 32);
   dim3 grid((unsigned)(GM_BWD_PERSIST ? std::min<int64_t>(units, device_cus()) : units));
 #define NAIS_GM_BWD(HBM, DC, HC, XC)                                                        \
   if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
-    hipLaunchKernelGGL((gm_backward_kernel<HBM, DC, HC, XC>), grid, dim3(GW * 64), lds, st, a, saved, \
-                       pred, gpred, g, bad_rows);                                          \
+    hipLaunchKernelGGL((gm_backward_kernel<HBM, DC, HC, XC, GWT>), grid, dim3(GWT * 64), lds, st, a, \
+                       saved, pred, gpred, g, bad_rows, sl0);                              \
     return nais_internal_check_launch("gm_backward_kernel");                               \
   }
   NAIS_GM_SHAPES_BWD(NAIS_GM_BWD)
 #undef NAIS_GM_BWD
   if (a.H > 64)
-    hipLaunchKernelGGL(gm_backward_kernel<4>, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g, bad_rows);
+    hipLaunchKernelGGL((gm_backward_kernel<4, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, saved,
+                       pred, gpred, g, bad_rows, sl0);
   else
-    hipLaunchKernelGGL(gm_backward_kernel<2>, grid, dim3(GW * 64), lds, st, a, saved, pred, gpred, g, bad_rows);
+    hipLaunchKernelGGL((gm_backward_kernel<2, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, saved,
+                       pred, gpred, g, bad_rows, sl0);
   return nais_internal_check_launch("gm_backward_kernel");
+}
+
+int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
+               const GGrads& g, hipStream_t st, const int32_t* bad_rows = nullptr) {
+  const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
+  const int64_t first = GM_BWD_PERSIST ? nsl : g_split_slices(a);
+  int rc = g_backward_launch<GW>(a, saved, pred, gpred, g, st, bad_rows, nrt * first, 0);
+  if (rc || first == nsl || NAIS_GM_TAIL <= 0) return rc;
+  constexpr int TW_ = NAIS_GM_TAIL > 0 ? NAIS_GM_TAIL : 1;
+  return g_backward_launch<TW_>(a, saved, pred, gpred, g, st, bad_rows, (a.b + TW_ - 1) / TW_, (int)first);
 }
 
 }  // namespace

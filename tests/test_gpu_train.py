@@ -353,6 +353,25 @@ def test_fused_step_matches_dropin(D, H):
     assert tr.finish() > 0
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_general_kernels_short_slice_split_config3(split, monkeypatch):
+    """Config-3 shape at the reference's D = H = 128 (1,020 rows x 204 history items, run.py:86,
+    837-838): the general kernels run the six full 32-item slices with 12-row workgroups and the
+    12-item last slice as a second launch of 4-row workgroups (g_split_slices, nais_train.hip:
+    85 x 7 = 595 units would take 3 rounds over 256 CUs, 510 take 2). Gradients and loss equal the
+    float64 oracle's with the split on and off (NAIS_GM_TAIL=0), dropout off."""
+    monkeypatch.setenv("NAIS_GM_TAIL", split)
+    P, D, H, n = 3000, 128, 128, 204
+    p = _params(P, D, H, 12)
+    hist, data, labels = _batch(P, n, 4, seed=3)
+    assert hist.shape == (1020, 204)
+    pred, loss, grads = _step(_model(p), hist, data, labels)
+    r = train_oracle.train_step_basic(p, hist, data, labels)
+    assert np.abs(pred - r["pred"]).max() <= SCORE_ATOL
+    assert abs(loss - r["loss"]) <= 1e-5
+    _assert_grads(grads, r["grads"])
+
+
 @pytest.mark.parametrize("wd", [0.0, 0.01])
 @pytest.mark.parametrize("D,H", [(32, 48), (128, 128), (80, 72)])
 def test_fused_step_oracle(wd, D, H):
@@ -369,6 +388,26 @@ def test_fused_step_oracle(wd, D, H):
     for k, q in m.named_parameters():
         want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), r["grads"][k].reshape(p[k].shape),
                                        0.02, 1, weight_decay=wd)
+        bad = ~np.isclose(q.detach().cpu().numpy(), want, rtol=1e-4, atol=2e-5)
+        assert bad.mean() <= 1e-3, (k, int(bad.sum()))
+
+
+def test_fused_step_config3_split_vs_oracle():
+    """NAISTrainer.step at the config-3 shape, D = H = 128 (the fused step's u cache and the split
+    general kernels together): loss and the Adagrad-updated parameters against the oracle."""
+    P, D, H, n = 3000, 128, 128, 204
+    p = _params(P, D, H, 13)
+    X = _csr(2, P, 10, seed=4)
+    m = _model(p)
+    tr = _trainer(m, X, lr=0.02)
+    hist, data, labels = _batch(P, n, 4, seed=5)
+    tr.step(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV), torch.as_tensor(labels).to(DEV))
+    loss = tr.finish()
+    r = train_oracle.train_step_basic(p, hist, data, labels)
+    assert abs(loss - r["loss"]) <= 1e-5
+    for k, q in m.named_parameters():
+        want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), r["grads"][k].reshape(p[k].shape),
+                                       0.02, 1)
         bad = ~np.isclose(q.detach().cpu().numpy(), want, rtol=1e-4, atol=2e-5)
         assert bad.mean() <= 1e-3, (k, int(bad.sum()))
 
