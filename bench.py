@@ -605,12 +605,23 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             el = float(t.item())
         per, nl = {}, {}
         for step_ev in evs:
+            ref = next((e0 for _, e0, _, _ in step_ev if e0 is not None), None)
+            spans = {}
             for kind, e0, e1, launches in step_ev:
                 if e0 is None:          # a setting, not a timed launch
                     per[kind] = launches
                     continue
-                per.setdefault(kind, []).append(e0.elapsed_time(e1))
+                spans.setdefault(kind, []).append((ref.elapsed_time(e0), ref.elapsed_time(e1)))
                 nl[kind] = nl.get(kind, 0) + launches
+            # busy time of each kind = the union of its launch intervals: the table launches of
+            # consecutive blocks overlap (two table streams, catalog.PAIR_TABLE_STREAMS)
+            for kind, iv in spans.items():
+                busy, end = 0.0, -1e30
+                for lo, hi in sorted(iv):
+                    if hi > end:
+                        busy += hi - max(lo, end)
+                        end = hi
+                per.setdefault(kind, []).append(busy)
         per["_launches"] = nl
         return el, per
 
@@ -811,6 +822,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                 "table_cus": table["cus"], "cu_layout": catalog.PAIR_CU_LAYOUT,
                 "block_cols": catalog.PAIR_BLOCK_COLS,
                 "first_table_all_cus": catalog.PAIR_FIRST_TABLE_ALL_CUS,
+                "table_streams": catalog.PAIR_TABLE_STREAMS,
                 "table_gather_frac": catalog.PAIR_TABLE_GATHER_FRAC,
                 "fused_topk": catalog.PAIR_FUSED_TOPK, "lpt_order": catalog.PAIR_LPT_ORDER,
                 **({"emulated_world_shard": emulate} if emulate > 1 and world == 1 else {}),

@@ -256,6 +256,10 @@ PAIR_TABLE_GATHER_FRAC = 0.0
 # wave keeps up to 32 users' sums of a 64-column chunk in registers while all waves walk the table
 # in blocks of PAIR_L2_ROWS rows (~1.5 MB), so the rows shared by ~50 users come from the XCD's L2
 # rather than the Infinity Cache. Same sums in the same order as nais_pair_gather_topk.
+# Table launches alternate over two streams with the same CU mask, so block b + 1's workgroups
+# fill the CUs that block b's last, partial round of workgroups leaves idle (1,564 workgroups of
+# one table block = 9.8 rounds over 160 CUs; one stream waits for the whole launch to drain).
+PAIR_TABLE_STREAMS = int(os.environ.get("NAIS_PAIR_TABLE_STREAMS", "2"))
 PAIR_L2_GATHER = os.environ.get("NAIS_PAIR_L2", "0") == "1"   # A/B knob, off: 2-3x slower
 PAIR_L2_ROWS = int(os.environ.get("NAIS_PAIR_L2_ROWS", "3072"))
 PAIR_L2_WAVES_PER_CU = int(os.environ.get("NAIS_PAIR_L2_WAVES_PER_CU", "20"))
@@ -304,7 +308,8 @@ def _destroy_masked_streams():
 
 
 def _masked_streams(dev, table_cus):
-    """(table stream, gather stream) as torch ExternalStreams over disjoint CU masks (cached)."""
+    """(table stream, gather stream, second table stream) as torch ExternalStreams: the two table
+    streams on one CU mask, the gather stream on the disjoint rest (cached)."""
     key = (str(dev), table_cus, PAIR_CU_LAYOUT)
     hit = _masked.get(key)
     if hit is not None:
@@ -316,7 +321,7 @@ def _masked_streams(dev, table_cus):
         mine = {int(i * n / table_cus) for i in range(table_cus)}
     words = (n + 31) // 32
     masks = []
-    for sel in (mine, set(range(n)) - mine):
+    for sel in (mine, set(range(n)) - mine, mine):
         m = (ctypes.c_uint32 * words)()
         for c in sel:
             m[c // 32] |= 1 << (c % 32)
@@ -505,12 +510,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             if prior is not None:
                 pr_of.update({id(t): torch.empty(J, W, dtype=torch.float64, device=dev) for t in tabs})
             if overlap:
-                ts, gs = _masked_streams(dev, table_cus)
+                ts, gs, ts2 = _masked_streams(dev, table_cus)
+                tss = (ts, ts2) if PAIR_TABLE_STREAMS > 1 else (ts,)
                 first_all = PAIR_FIRST_TABLE_ALL_CUS
                 if first_all:      # block 0's table alone, on the caller's stream (all CUs)
                     w0 = min(W, c1_all - blocks[0])
                     timed("table", lambda: table(tabs[0], blocks[0], w0, st))
-                ts.wait_stream(torch_stream)
+                for t_ in tss:
+                    t_.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
                 done_g = [None, None]
                 # launch slots [m1, m) are gathered on the table stream (PAIR_TABLE_GATHER_FRAC)
@@ -527,13 +534,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 w = min(W, c1_all - c0)
                 tab = tabs[b % len(tabs)]
                 if overlap:
+                    tsb = tss[b % len(tss)]
                     if done_g[b % 2] is not None:
-                        ts.wait_event(done_g[b % 2])     # buffer free: its gather finished
+                        tsb.wait_event(done_g[b % 2])    # buffer free: its gather finished
                     if not (b == 0 and first_all):
                         e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e_t0.record(ts)
-                        table(tab, c0, w, ts.cuda_stream)
-                        e_t1.record(ts)
+                        e_t0.record(tsb)
+                        table(tab, c0, w, tsb.cuda_stream)
+                        e_t1.record(tsb)
                         gs.wait_event(e_t1)
                         if events is not None:
                             events.append(("table", e_t0, e_t1, 1))
@@ -545,16 +553,17 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     if events is not None:
                         events.append(("gather", e_g0, e_g1, gather_launches(w)))
                     if m1 < m:   # the tail users, behind this block's table on the table stream
-                        gather(tab, c0, w, ts.cuda_stream, m1, m)
+                        gather(tab, c0, w, tsb.cuda_stream, m1, m)
                     continue
                 timed("table", lambda: table(tab, c0, w, st))
                 timed("gather", lambda: gather(tab, c0, w, st), gather_launches(w))
             if overlap:
                 torch_stream.wait_stream(gs)
-                torch_stream.wait_stream(ts)
+                for t_ in tss:
+                    torch_stream.wait_stream(t_)
                 for t in [*tabs, *pr_of.values()]:   # not handed to the main stream early
-                    t.record_stream(ts)
-                    t.record_stream(gs)
+                    for t_ in (*tss, gs):
+                        t.record_stream(t_)
             del tabs
             pr_of.clear()
             if not fused:
