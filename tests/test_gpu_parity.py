@@ -541,6 +541,8 @@ def test_pairs_auto_choice_and_new4():
 
 @pytest.mark.parametrize("knobs", [
     {"PAIR_BLOCK_COLS": 256},                                   # many blocks, overlapped
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_STREAMS": 1},          # one table stream
+    {"PAIR_BLOCK_COLS": 256, "PAIR_FIRST_TABLE_ALL_CUS": False, "PAIR_TABLE_STREAMS": 2},
     {"PAIR_BLOCK_COLS": 768, "PAIR_FIRST_TABLE_ALL_CUS": False},
     {"PAIR_TABLE_CUS": 0},                                      # serial, one stream
     {"PAIR_MEMORY_FRACTION": 2e-6},                             # minimum block width
