@@ -286,8 +286,9 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
 int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int64_t* items,
                               int64_t num_items, int64_t col0, int64_t cols, double a, double b,
                               double* pr, int64_t ld, void* stream);
-#define NAIS_PRIOR_FINITE 1   /* flags: every pr entry is finite (a and a * max(0.01, d)^b finite for
-                                 every distance): a product that underflowed to 0.0 stays 0.0, so
+#define NAIS_PRIOR_FINITE 1   /* flags: every pr entry is finite and >= +0 (a > 0, a * max(0.01, d)^b
+                                 finite for every distance): a product that underflowed to +0.0
+                                 stays +0.0, so
                                  the gather stops reading a wave's rows once all its columns are 0 */
 int32_t nais_pair_prior_gather(const double* pr, int64_t ld, const int32_t* rowmap,
                                const int64_t* indptr, const int64_t* indices, const int32_t* users,

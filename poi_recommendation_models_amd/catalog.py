@@ -520,6 +520,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     t_.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
                 done_g = [None, None]
+                done_tail = None   # the previous block's tail gather (another table stream)
                 # launch slots [m1, m) are gathered on the table stream (PAIR_TABLE_GATHER_FRAC)
                 m1 = m
                 if fused and PAIR_TABLE_GATHER_FRAC > 0 and m > 1:
@@ -553,7 +554,13 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     if events is not None:
                         events.append(("gather", e_g0, e_g1, gather_launches(w)))
                     if m1 < m:   # the tail users, behind this block's table on the table stream
+                        # their running top-k keys were last merged by the previous block's tail
+                        # gather, on the other table stream: order the two merges
+                        if done_tail is not None and len(tss) > 1:
+                            tsb.wait_event(done_tail)
                         gather(tab, c0, w, tsb.cuda_stream, m1, m)
+                        done_tail = torch.cuda.Event()
+                        done_tail.record(tsb)
                     continue
                 timed("table", lambda: table(tab, c0, w, st))
                 timed("gather", lambda: gather(tab, c0, w, st), gather_launches(w))
@@ -613,11 +620,12 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
 
 def _prior_entries_finite(a, b):
     """Every pr_d(d) = a * max(0.01, d)^b (powerLaw.py:86-88) is finite for 0 <= d <= half the
-    earth's circumference (the range of powerLaw.dist), so a G product that reached 0.0 stays 0.0
-    (nais_pair_prior_gather's NAIS_PRIOR_FINITE)."""
+    earth's circumference (the range of powerLaw.dist), and with a > 0 every factor is >= +0, so a
+    G product that reached +0.0 stays +0.0, sign bit included (nais_pair_prior_gather's
+    NAIS_PRIOR_FINITE; the per-user prior_kernel's twin is prior_zero_exit in nais_kernels.hip)."""
     import math
     a, b = float(a), float(b)
-    if not (math.isfinite(a) and math.isfinite(b)):
+    if not (math.isfinite(a) and math.isfinite(b) and a > 0.0):
         return False
     try:
         ends = (a * 0.01 ** b, a * (math.pi * 6371.0) ** b)

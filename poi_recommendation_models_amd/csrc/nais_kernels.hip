@@ -24,6 +24,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <type_traits>
 #include <string>
 
@@ -1995,10 +1997,13 @@ constexpr int PRIOR_JC = 256;
 
 // G[slot][c] = prod_j pr_d(dist(coo_j, coo_c)) over the user's history in CSR order
 // (np.prod, powerLaw.py:92); history POIs get -1. gmax[slot] = max over candidates (u64 bits).
+// zero_exit (prior_zero_exit(a, b)): long histories underflow G to 0.0 after ~110 POIs at city
+// distances; the remaining factors are then not evaluated (bit-identical, see the loop).
 __global__ void __launch_bounds__(PRIOR_THREADS)
 prior_kernel(const double* __restrict__ coords, int64_t P, const int64_t* __restrict__ indptr,
              const int64_t* __restrict__ indices, const int32_t* __restrict__ users, double pa,
-             double pb, double* __restrict__ G, int64_t ld, unsigned long long* __restrict__ gmax) {
+             double pb, double* __restrict__ G, int64_t ld, unsigned long long* __restrict__ gmax,
+             int zero_exit) {
   __shared__ Geo hg[PRIOR_JC];
   __shared__ int32_t hid[PRIOR_JC];
   __shared__ double red[PRIOR_THREADS / 64];
@@ -2021,7 +2026,9 @@ prior_kernel(const double* __restrict__ coords, int64_t P, const int64_t* __rest
     }
     __syncthreads();
     for (int jj = 0; jj < jn; ++jj) {
-      g = __dmul_rn(g, ref_pr_d(pa, pb, ref_dist(hg[jj], gc)));
+      // zero_exit: a product that reached +0.0 stays +0.0 (every factor finite and >= +0), so
+      // the f64 haversine + pow is skipped -- for the whole wave once all its lanes are there
+      if (!zero_exit || g != 0.0) g = __dmul_rn(g, ref_pr_d(pa, pb, ref_dist(hg[jj], gc)));
       in_hist |= hid[jj] == (int32_t)c;
     }
   }
@@ -2597,6 +2604,20 @@ int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Every pr_d(d) = a * max(0.01, d)^b is finite and >= +0 for d in powerLaw.dist's range
+// [0, pi * 6371] (a NaN distance takes the 0.01 branch): a > 0 and both ends finite (pr_d is
+// monotone in d). Then a G product at +0.0 stays +0.0. The host-side twin for the pairs route is
+// catalog._prior_entries_finite. NAIS_PRIOR_EXIT=0 turns the exit off (A/B).
+bool prior_zero_exit(double a, double b) {
+  static const bool on = [] {
+    const char* e = std::getenv("NAIS_PRIOR_EXIT");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || !std::isfinite(a) || !std::isfinite(b) || !(a > 0.0)) return false;
+  const double lo = a * std::pow(0.01, b), hi = a * std::pow(3.141592653589793 * 6371.0, b);
+  return std::isfinite(lo) && std::isfinite(hi);
+}
+
 int launch_prior(const double* coords, int64_t P, const int64_t* indptr, const int64_t* indices,
                  const int32_t* users, int nb, double a, double b, double* G, int64_t ld,
                  unsigned long long* gmax, hipStream_t st) {
@@ -2604,7 +2625,7 @@ int launch_prior(const double* coords, int64_t P, const int64_t* indptr, const i
   if (e != hipSuccess) return fail(NAIS_E_HIP, std::string("memset: ") + hipGetErrorString(e));
   dim3 grid((unsigned)((P + PRIOR_THREADS - 1) / PRIOR_THREADS), (unsigned)nb);
   hipLaunchKernelGGL(prior_kernel, grid, dim3(PRIOR_THREADS), 0, st, coords, P, indptr, indices,
-                     users, a, b, G, ld, gmax);
+                     users, a, b, G, ld, gmax, prior_zero_exit(a, b) ? 1 : 0);
   return check_launch("prior_kernel");
 }
 

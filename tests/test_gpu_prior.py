@@ -98,18 +98,21 @@ def test_score_topk_with_prior_blend(strategy):
                                    lookup=dict(zip(cand.tolist(), blended.tolist())))
 
 
-@pytest.mark.parametrize("h_max,flags", [(60, 0), (60, 1), (240, 0), (240, 1)])
-def test_pair_prior_gather_equals_prior_rows_bits(h_max, flags):
+@pytest.mark.parametrize("h_max,flags,a", [(60, 0, 0.052), (60, 1, 0.052), (240, 0, 0.052),
+                                           (240, 1, 0.052), (240, 0, -0.052)])
+def test_pair_prior_gather_equals_prior_rows_bits(h_max, flags, a):
     """The pairs route's G (nais_pair_prior_table + nais_pair_prior_gather, several column blocks)
     is bit-identical to nais_powerlaw_prior's rows (the direct route), and so is the per-user max --
     also with the underflow exit (flags = NAIS_PRIOR_FINITE) on histories long enough (h up to 240)
-    that whole stripes of G underflow to 0.0 (np.prod's own result, powerLaw.py:92)."""
+    that whole stripes of G underflow to 0.0 (np.prod's own result, powerLaw.py:92). flags = 0
+    computes every factor, so the (240, 0) case also pins prior_kernel's own underflow exit
+    (prior_zero_exit) bit for bit; a < 0 (signed zeros: the exit must be off) pins its guard."""
     from poi_recommendation_models_amd import _capi
     from poi_recommendation_models_amd.catalog import DeviceCSR, prior_rows
     from poi_recommendation_models_amd.synthetic import make_checkins
     data = make_checkins(40, 1500, h_max, seed=8)
     P, U = data.num_pois, data.num_users
-    a, b = 0.052, -1.37
+    b = -1.37
     dev = torch.device(DEV)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, dev)
     ref, ref_max = prior_rows(csr, range(U), a, b, data.place_coords, dev)
@@ -140,7 +143,7 @@ def test_pair_prior_gather_equals_prior_rows_bits(h_max, flags):
     torch.cuda.synchronize()
     assert torch.equal(G.view(torch.int64), ref.view(torch.int64))
     assert torch.equal(gmax, ref_max.view(torch.int64))
-    if h_max > 200:   # the case the exit is for: some users' whole rows underflowed
+    if h_max > 200 and a > 0:   # the case the exit is for: some users' whole rows underflowed
         assert bool(((G == 0) | (G == -1)).all(dim=1).any())
 
 
