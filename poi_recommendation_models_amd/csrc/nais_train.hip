@@ -1100,18 +1100,25 @@ __device__ __forceinline__ float half_sum(float v) {
 // backward's)
 template <int HBM, int DC = 0, int HC = 0, int XC = 0, int GWT = GW>
 __global__ void __launch_bounds__(GWT * 64)
-gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np, int32_t sl0) {
+gm_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np, int32_t sl0, int32_t trows) {
   extern __shared__ float4 glds4[];
   float* Lb = reinterpret_cast<float*>(glds4);
   const GS s = make_gs<DC, HC, XC>(a);
   const GL g(s.D, s.H, s.DIN, GWT);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
   // persistent: W1 staged once, then work units (row tile of GWT rows, slice of 32 items), row
-  // tile fastest, strided over the grid
+  // tile fastest, strided over the grid. trows > 0: the short last slice's units are tiles of
+  // trows rows (waves >= trows idle in them), so they spread over more workgroups' last round
   gm_stage_w<GWT>(a, s, g, Lb, tid);
-  const int64_t nrt = (a.b + GWT - 1) / GWT, units = nrt * ((a.n + 31) / 32 - sl0);
+  const int64_t nrt = (a.b + GWT - 1) / GWT, nsl = (a.n + 31) / 32 - sl0;
+  const int64_t nrt_t = trows > 0 ? (a.b + trows - 1) / trows : 0;
+  const int64_t ufull = trows > 0 ? nrt * (nsl - 1) : nrt * nsl;
+  const int64_t units = ufull + (trows > 0 ? nrt_t : 0);
   for (int64_t un = blockIdx.x; un < units; un += gridDim.x) {
-    const int64_t sl = sl0 + un / nrt, c0 = (un % nrt) * GWT, c = c0 + w;
+    const bool tu = un >= ufull;
+    const int64_t sl = tu ? sl0 + nsl - 1 : sl0 + un / nrt;
+    const int64_t c0 = tu ? (un - ufull) * trows : (un % nrt) * GWT;
+    const int64_t c = (tu && w >= trows) ? a.b : c0 + w;   // idle waves: past the last row
     const int64_t j0 = sl * 32;
     const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
     __syncthreads();   // the previous unit's operand reads are done
@@ -1595,7 +1602,8 @@ int device_cus() {
 #define NAIS_GM_SHAPES_BWD(X) X(4, 128, 128, 0) X(2, 64, 64, 0) X(2, 64, 64, 2)
 
 template <int GWT>
-int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64_t units, int sl0) {
+int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64_t units, int sl0,
+                     int trows = 0) {
   const size_t lds = g_lds_bytes(a, false, GWT);
 #define NAIS_GM_LDS(HBM, DC, HC, XC) set_lds(gm_forward_kernel<HBM, DC, HC, XC, GWT>, 160 * 1024),
   static bool once = (NAIS_GM_SHAPES(NAIS_GM_LDS) set_lds(gm_forward_kernel<4, 0, 0, 0, GWT>, 160 * 1024),
@@ -1607,15 +1615,17 @@ int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64
 #define NAIS_GM_FWD(HBM, DC, HC, XC)                                                        \
   if (a.D == DC && a.H == HC && a.DIN == DC + XC) {                                        \
     hipLaunchKernelGGL((gm_forward_kernel<HBM, DC, HC, XC, GWT>), grid, dim3(GWT * 64), lds, st, a, \
-                       Sp, Np, sl0);                                                       \
+                       Sp, Np, sl0, trows);                                                \
     return nais_internal_check_launch("gm_forward_kernel");                                \
   }
   NAIS_GM_SHAPES(NAIS_GM_FWD)
 #undef NAIS_GM_FWD
   if (a.H > 64)
-    hipLaunchKernelGGL((gm_forward_kernel<4, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0);
+    hipLaunchKernelGGL((gm_forward_kernel<4, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0,
+                       trows);
   else
-    hipLaunchKernelGGL((gm_forward_kernel<2, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0);
+    hipLaunchKernelGGL((gm_forward_kernel<2, 0, 0, 0, GWT>), grid, dim3(GWT * 64), lds, st, a, Sp, Np, sl0,
+                       trows);
   return nais_internal_check_launch("gm_forward_kernel");
 }
 
@@ -1642,9 +1652,19 @@ int64_t g_split_slices(const GArgs& a) {
 // The forward stays one persistent launch: its workgroups stage W1 once for all their units, so
 // the short slice's units ride on workgroups that already hold it (A/B, config 3 at D = H = 128:
 // split 0.129 ms vs 0.110 ms -- a 4-row tail workgroup pays a whole W1 staging for one unit).
+// Inside that launch the short slice's units are NAIS_GM_TAIL-row tiles when the backward splits
+// (same criterion, g_split_slices): config 3's 85 twelve-row short units become 255 four-row ones,
+// one per workgroup's last round instead of a full-length third round on 85 of them.
+// NAIS_GM_FWD_TAIL=0: twelve-row short units (A/B).
 int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
   const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
-  return g_forward_launch<GW>(a, Sp, Np, st, nrt * nsl, 0);
+  static const bool fwd_tail = [] {
+    const char* e = getenv("NAIS_GM_FWD_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  const int trows = (fwd_tail && NAIS_GM_TAIL > 0 && g_split_slices(a) < nsl) ? NAIS_GM_TAIL : 0;
+  const int64_t units = trows > 0 ? nrt * (nsl - 1) + (a.b + trows - 1) / trows : nrt * nsl;
+  return g_forward_launch<GW>(a, Sp, Np, st, units, 0, trows);
 }
 
 template <int GWT>
