@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather-leg", action="store_true",
                     help="skip the standalone history-gather leg (nais_gather_rows, 2 GB table)")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the config-3 training-step leg (fused / drop-in / eager torch, D=H=64 and 128)")
     ap.add_argument("--no-self-check", action="store_true",
                     help="skip the oracle check of 2 bench users' top-50 after the timed steps")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -277,6 +279,144 @@ def gather_rows_leg(dev, lib, traffic_json, rows=4_000_000, dim=128, m=4_000_000
             "index_pattern": "random permutation (each row read once)", "rows_bit_exact": ok}
 
 
+class EagerNAIS(torch.nn.Module):
+    """The reference's NAIS_basic training forward (model.py:57-89: gather, h * t, attn_layer1,
+    Dropout, ReLU, attn_layer2, exp, mask, pow(beta), divide, bmm, sigmoid) in eager PyTorch ops
+    with autograd -- what run.py:101-109 runs when handed a ROCm device. Baseline timing only."""
+
+    def __init__(self, src):
+        super().__init__()
+        cp = lambda t: torch.nn.Parameter(t.detach().clone())
+        self.eh, self.et = cp(src.embed_history.weight), cp(src.embed_target.weight)
+        self.w1, self.b1 = cp(src.attn_layer1.weight), cp(src.attn_layer1.bias)
+        self.w2 = cp(src.attn_layer2.weight)
+        self.drop = torch.nn.Dropout(src.drop.p)
+        self.beta = src.beta
+
+    def forward(self, hist, tgt):
+        F = torch.nn.functional
+        h = F.embedding(hist, self.eh)
+        t = F.embedding(tgt, self.et).reshape(len(tgt), 1, -1)
+        r1 = torch.relu(self.drop(F.linear(h * t, self.w1, self.b1)))
+        a = torch.exp(F.linear(r1, self.w2)).squeeze(-1) * (hist != tgt.reshape(-1, 1))
+        s = torch.pow(a.sum(-1), self.beta)
+        w = torch.divide(a.T, s).T.reshape(len(tgt), -1, 1)
+        return torch.sigmoid(torch.bmm(h * w, t.reshape(len(tgt), -1, 1)).squeeze(-1).sum(-1))
+
+
+def train_batches(P, n, num_ng, count, seed):
+    """get_NAIS_batch-shaped batches (batches.py:24-50): n shuffled positives shared as the
+    history of n * (1 + num_ng) rows [pos, neg x num_ng], labels 1 / 0."""
+    r = np.random.default_rng(seed)
+    out = []
+    for _ in range(count):
+        pos = r.choice(P, n, replace=False)
+        neg = r.choice(np.setdiff1d(np.arange(P), pos), n * num_ng, replace=False)
+        data = np.concatenate([pos.reshape(-1, 1), neg.reshape(n, num_ng)], 1).reshape(-1)
+        labels = np.concatenate([np.ones((n, 1)), np.zeros((n, num_ng))], 1).reshape(-1)
+        out.append((pos, data, labels.astype(np.float32)))
+    return out
+
+
+def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=True):
+    """BASELINE config 3 (run.py:91-109): one NAIS_basic training step on a get_NAIS_batch batch
+    of n * (1 + num_ng) = 1,020 rows x 204 history items, P = 100k POIs, dropout 0.5, Adagrad
+    lr 0.01. ms per step of (1) the fused native step (NAISTrainer.step: forward + BCELoss +
+    backward + Adagrad in one C-ABI call), (2) the drop-in loop run.py runs (model(...),
+    loss_func, backward(), optim.Adagrad.step()), (3) the reference's op sequence in eager
+    PyTorch + torch.optim.Adagrad on the same GPU. Self-check: one fused step from fresh
+    parameters against oracle/train_oracle.py (float64) with the device's dropout mask injected:
+    the loss within 1e-5 and every updated parameter (all P rows) within rtol 1e-4."""
+    import scipy.sparse as sp
+    from poi_recommendation_models_amd import _capi, optim
+    from poi_recommendation_models_amd.model import NAIS_basic
+    from poi_recommendation_models_amd.trainer import NAISTrainer
+    torch.manual_seed(0)
+    m = NAIS_basic(P, D, H, 0.5)
+    with torch.no_grad():   # trained-like embedding scale: the attention is not uniform
+        m.embed_history.weight.normal_(0, 0.3)
+        m.embed_target.weight.normal_(0, 0.3)
+    m = m.to(dev).train()
+    m.drop.p = 0.5
+    m.report_nan = False              # the reference prints NaN counts (a .item() sync per call)
+    m.check_shared_history = False    # batches are get_NAIS_batch-shaped by construction
+    host = train_batches(P, n, num_ng, 8, seed=1)
+    bs = [(torch.as_tensor(np.repeat(h[None], len(d), 0)).to(dev), torch.as_tensor(d).to(dev),
+           torch.as_tensor(l).to(dev)) for h, d, l in host]
+    p0 = {k: v.detach().cpu().numpy().copy() for k, v in m.named_parameters()}
+
+    def loop(fn):
+        for i in range(warmup):
+            fn(*bs[i % len(bs)])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(*bs[i % len(bs)])
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    out = {"what": "config3 NAIS_basic training step: %d rows x %d history items, P = %d, D = %d, "
+                   "H = %d, dropout 0.5, Adagrad" % (n * (1 + num_ng), n, P, D, H),
+           "steps": steps, "warmup": warmup}
+    rows = np.repeat(np.arange(len(host)), n)
+    X = sp.csr_matrix((np.ones(len(rows)), (rows, np.concatenate([np.sort(h) for h, _, _ in host]))),
+                      shape=(len(host), P))
+    # (1) fused step, from fresh parameters: its first step is the self-checked one
+    tr = NAISTrainer(m, X, lr=0.01, num_ng=num_ng)
+    seed = 20240611
+    tr.step(bs[0][0][0], bs[0][1], bs[0][2], dropout_seed=seed)
+    loss0 = tr.finish()
+    p1 = {k: v.detach().cpu().numpy().copy() for k, v in m.named_parameters()}
+    out["fused_ms_per_step"] = loop(lambda h, d, l: tr.step(h[0], d, l))
+    tr.finish()
+    # (2) the drop-in loop
+    opt = optim.Adagrad(m.parameters(), lr=0.01)
+    m.loss_func.check_input = False     # finite by construction (no single-item histories)
+
+    def dropin(h, d, l):
+        opt.zero_grad()
+        m.loss_func(m(h, d), l).backward()
+        opt.step()
+    out["dropin_ms_per_step"] = loop(dropin)
+    # (3) eager PyTorch, the reference's ops
+    em = EagerNAIS(m).to(dev).train()
+    eopt = torch.optim.Adagrad(em.parameters(), lr=0.01)
+    bce = torch.nn.BCELoss()
+
+    def eager(h, d, l):
+        eopt.zero_grad()
+        bce(em(h, d), l).backward()
+        eopt.step()
+    out["torch_eager_ms_per_step"] = loop(eager)
+    out["fused_speedup_vs_eager"] = out["torch_eager_ms_per_step"] / out["fused_ms_per_step"]
+    out["dropin_speedup_vs_eager"] = out["torch_eager_ms_per_step"] / out["dropin_ms_per_step"]
+    if check:
+        from oracle import train_oracle
+        t0 = time.perf_counter()
+        b = len(host[0][1])
+        keep = torch.empty(b * n * H, dtype=torch.uint8, device=dev)
+        _capi.check(_capi.load().nais_dropout_mask(seed, b, n, H, 0.5, keep.data_ptr(),
+                                                   _capi.stream_handle(dev)), "nais_dropout_mask")
+        keep = keep.view(b, n, H).cpu().numpy()
+        h, d, l = host[0]
+        r = train_oracle.train_step_basic(p0, np.repeat(h[None], b, 0), d, l, keep=keep, drop_p=0.5)
+        worst, bad = 0.0, 0
+        for k, v in p0.items():
+            want, _ = train_oracle.adagrad(v, np.zeros_like(v), r["grads"][k].reshape(v.shape), 0.01, 1)
+            miss = ~np.isclose(p1[k], want, rtol=1e-4, atol=2e-5)
+            bad += int(miss.sum())
+            worst = max(worst, float(miss.mean()))
+        out["self_check"] = {"oracle": "oracle/train_oracle.py (float64, dropout mask injected)",
+                             "loss": loss0, "oracle_loss": float(r["loss"]),
+                             "loss_ok": abs(loss0 - float(r["loss"])) <= 1e-5,
+                             "params_off_rtol_1e-4": bad, "worst_fraction_off": worst,
+                             "params_ok": worst <= 1e-3,
+                             "seconds": round(time.perf_counter() - t0, 1)}
+    del tr, opt, em, eopt, m
+    torch.cuda.empty_cache()
+    return out
+
+
 def self_launch(a):
     """--gpus N > 1 without a torchrun environment: start N fresh worker processes through
     torch.distributed.run (this process never touches the GPU) and return their exit code."""
@@ -421,12 +561,8 @@ def main():
             if ev is not None:
                 ev[2].record(stream)
             if world > 1:   # the per-step exchange: every rank's top-k blocks
-                if a.backend == "nccl":
-                    dist.all_gather_into_tensor(gat_ids, ids)
-                    dist.all_gather_into_tensor(gat_sc, top)
-                else:
-                    dist.all_gather(list(gat_ids.chunk(world)), ids)
-                    dist.all_gather(list(gat_sc.chunk(world)), top)
+                dist.all_gather_into_tensor(gat_ids, ids)
+                dist.all_gather_into_tensor(gat_sc, top)
 
         for s in range(nwarm):
             step(s)
@@ -584,21 +720,23 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         def job(events=None):
             return distributed_topk_pairs(model, csr, users, K, group=group, events=events)
 
-    def run(precision, nwarm, nsteps):
+    def run(precision, nwarm, nsteps, fn=None):
+        fn = fn or job
         model.precision = precision
         for _ in range(nwarm):
-            job()
+            fn()
         evs = [[] for _ in range(nsteps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(nsteps):
-            last["out"] = job(evs[i])
+            last["out"] = fn(evs[i])
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        last["wall_ms"] = el / nsteps * 1e3
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -626,6 +764,22 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         return el, per
 
     elapsed, per = run(a.precision, a.warmup, a.steps)
+    wall_ms = last["wall_ms"]
+    ranks = None
+    if world > 1:   # every rank's phase busy times (ms per step), gathered over the same group
+        ph = ("table", "gather", "allgather", "merge", "topk")
+        mine = torch.tensor([sum(per.get(kind, [])) / a.steps for kind in ph] + [wall_ms],
+                            dtype=torch.float64, device=dev)
+        allr = torch.empty(world * len(mine), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allr, mine)
+        allr = allr.view(world, -1).cpu().numpy()
+        ranks = {"world_size_reported": dist.get_world_size(), "backend": dist.get_backend(),
+                 "phases": ph + ("wall",),
+                 "ms_per_step_by_rank": [[round(float(x), 3) for x in row] for row in allr],
+                 "note": "busy time (union of launch intervals, HIP events) of each phase per step on "
+                         "each rank; allgather = the two all_gather_into_tensor calls of the [users, 50] "
+                         "blocks, merge = the top-k over world x 50 candidates; wall = this rank's own "
+                         "timed region / steps (value uses the max over ranks)"}
     pairs_job = float((P - hist_len[users]).sum())            # every user's whole catalog
     if emulate > 1 and world == 1:
         c0, c1 = column_blocks(P, emulate)[0]
@@ -749,9 +903,21 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                           "table_peak_tflops": t_l["peak"], "table_cus": t_l["cus"],
                           "gather_ms_per_step": g_l["ms_per_step"], "self_check": leg_check}
         model.precision = a.precision
-        legs["prior"], pr_out = variant_leg("prior", lambda: _score_topk_pairs(
-            model, csr, users, K, None, None, None, None, force=True,
-            prior=(PRIOR_A, PRIOR_B, PRIOR_ALPHA, data.place_coords)), a.leg_steps, pairs_job, dev)
+        def prior_job(events=None):
+            return _score_topk_pairs(model, csr, users, K, None, None, None, None, force=True,
+                                     events=events, prior=(PRIOR_A, PRIOR_B, PRIOR_ALPHA, data.place_coords))
+        el_p, per_p = run(a.precision, 1, a.leg_steps, prior_job)
+        pr_out = last["out"]
+        legs["prior"] = {"value": pairs_job * a.leg_steps / el_p, "unit": "pairs/s", "steps": a.leg_steps,
+                         "warmup": 1, "ms_per_step": el_p / a.leg_steps * 1e3,
+                         # the plan of the timed jobs (identical every step: the pass split is sized
+                         # from the memory this process can allocate, cached blocks included)
+                         "plan": {key: per_p.get(key) for key in (
+                             "passes", "users_per_pass", "block_cols", "distinct_rows", "table_cus",
+                             "usable_bytes", "budget_bytes")},
+                         "table_ms_per_step": sum(per_p.get("table", [])) / a.leg_steps,
+                         "gather_ms_per_step": sum(per_p.get("gather", [])) / a.leg_steps,
+                         "blend_topk_ms_per_step": sum(per_p.get("topk", [])) / a.leg_steps}
         if not a.no_self_check:   # a short-history user: the pure-Python prior is O(h x P)
             pu = int(np.argmin(np.abs(hist_len - 12)))
             legs["prior"]["self_check"] = prior_self_check(
@@ -785,6 +951,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     if world == 1 and not a.no_gather_leg:
         from poi_recommendation_models_amd import _capi
         legs["gather_rows"] = gather_rows_leg(dev, _capi.load(), a.traffic_json)
+    if world == 1 and not a.no_train_leg:
+        legs["train_step"] = {"D=H=%d" % d: train_leg(dev, d, d, check=not a.no_self_check)
+                              for d in (64, 128)}
     check = None
     if emulate == 1 and not a.no_self_check and rank == 0:   # N > 1: the merged top-k
         ids, sc = (t.cpu().numpy() for t in last["out"])
@@ -801,6 +970,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "metric": "scored (user,POI) pairs/sec full-catalog + top-50, %s POIs"
                       % {2: "50k", 4: "100k", 5: "1M"}[a.config],
             "value": pairs_job * a.steps / elapsed,
+            "per_rank": ranks,
             "unit": "pairs/s",
             "n_gpus": world,
             "steps": a.steps,
@@ -839,6 +1009,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "prior_path": legs.get("prior"),
             "region_distance_path": legs.get("region_distance"),
             "gather_rows_path": legs.get("gather_rows"),
+            "train_step_path": legs.get("train_step"),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -407,8 +407,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     entries = int(csr.hist_len[users].sum())
     if not force and (J == 0 or entries < PAIR_MIN_SHARING * J):
         return None
-    free = torch.cuda.mem_get_info(dev)[0]
-    budget = int(free * PAIR_MEMORY_FRACTION)
+    usable = usable_device_bytes(dev)
+    budget = int(usable * PAIR_MEMORY_FRACTION)
     from .model import _NAISDevice
     if prior is not None and (rows_only or model._pairs_only):
         raise NotImplementedError("the pairs route blends the prior over the rows of NAIS models only")
@@ -432,10 +432,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                                  stream_)
         else:
             model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
-                              tab[1].data_ptr(), W, stream_)
+                              tab[1].data_ptr(), ld, stream_)
         if prior is not None:
             _capi.check(lib.nais_pair_prior_table(pri_coords.data_ptr(), P, items.data_ptr(), J, c0, w,
-                                                  float(pa), float(pb), pr_of[id(tab)].data_ptr(), W,
+                                                  float(pa), float(pb), pr_of[id(tab)].data_ptr(), ld,
                                                   stream_), "nais_pair_prior_table")
     # users per pass: their score rows (+ float64 G rows with a prior) take at most half the
     # budget (fused: no score rows)
@@ -444,6 +444,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if prior is not None and group is not None:     # the same passes (and collectives) on every rank
         from .sharding import agree_min
         per_pass = agree_min(per_pass, dev, group)
+    if events is not None:    # the plan of this call, for the bench record
+        npass = (n + per_pass - 1) // per_pass
+        events.extend((name, None, None, v) for name, v in (
+            ("passes", npass), ("users_per_pass", per_pass), ("distinct_rows", J),
+            ("usable_bytes", usable), ("budget_bytes", budget)))
     keys_out = torch.empty(n, k, dtype=torch.float64, device=dev) if return_keys else None
     ids_out = torch.empty(n, k, dtype=torch.int32, device=dev)
     sc_out = torch.empty(n, k, dtype=torch.float32, device=dev)
@@ -471,7 +476,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         PAIR_L2_ROWS, gather_waves, stream_), "nais_pair_gather_topk_l2")
                     return
                 _capi.check(lib.nais_pair_gather_topk(
-                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta), k,
                     keys.data_ptr() + 8 * k * a, kcount.data_ptr() + 4 * a, counters[0:1].data_ptr(),
                     stream_), "nais_pair_gather_topk")
@@ -483,32 +488,36 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
 
             def gather(tab, c0, w, stream_, a=0, b=None):
                 _capi.check(lib.nais_pair_gather(
-                    tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, float(model.beta),
                     scores.data_ptr(), NC, c0_all, counters[0:1].data_ptr(), stream_), "nais_pair_gather")
                 if prior is not None:
                     _capi.check(lib.nais_pair_prior_gather(
-                        pr_of[id(tab)].data_ptr(), W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                        pr_of[id(tab)].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
                         csr.indices.data_ptr(), u_dev.data_ptr(), m, c0, w, G.data_ptr(), NC, c0_all,
                         gmax.data_ptr(), prior_flags, stream_), "nais_pair_prior_gather")
         if J > 0:
             # two f32 tables (+ the f64 pr_d table with a prior) per buffer, <= budget / 4 each
             W = min(PAIR_BLOCK_COLS, (budget // 4) // ((16 if prior is not None else 8) * J))
             W = int(min(NC, max(256, W // 256 * 256)))
+            # row pitch of the tables: a multiple of 4 floats (the gathers' 16-byte loads) even
+            # when a narrow column shard makes the block width odd
+            ld = (W + 3) // 4 * 4
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
             table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None) if PAIR_TABLE_CUS < 0
                          else PAIR_TABLE_CUS)
             if events is not None:
                 events.append(("table_cus", None, None, table_cus))
+                events.append(("block_cols", None, None, W))
             overlap = (0 < table_cus < ncu and len(blocks) > 1 and stream is None
                        and not no_side_streams)
             gather_waves = (ncu - table_cus if overlap else ncu) * PAIR_L2_WAVES_PER_CU
-            shape = ((W + 63) // 64, J, 128) if l2 else (2, J, W)
+            shape = ((W + 63) // 64, J, 128) if l2 else (2, J, ld)
             tabs = [torch.empty(*shape, dtype=torch.float32, device=dev)
                     for _ in range(2 if overlap else 1)]
             if prior is not None:
-                pr_of.update({id(t): torch.empty(J, W, dtype=torch.float64, device=dev) for t in tabs})
+                pr_of.update({id(t): torch.empty(J, ld, dtype=torch.float64, device=dev) for t in tabs})
             if overlap:
                 ts, gs, ts2 = _masked_streams(dev, table_cus)
                 tss = (ts, ts2) if PAIR_TABLE_STREAMS > 1 else (ts,)
@@ -616,6 +625,16 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     if return_keys:
         return ids, sc_out, keys_out
     return ids, sc_out
+
+
+def usable_device_bytes(dev):
+    """Bytes this process can still allocate on `dev`: the driver's free memory plus what torch's
+    caching allocator holds reserved but unused. The pass split of the pairs route is sized from
+    this, so it does not depend on how much of an earlier call's memory the allocator still caches
+    (mem_get_info alone counts that as used: the prior route's 60 GB of score + G rows at config 4
+    then fit one pass on a fresh process and needed two after a first job)."""
+    free = torch.cuda.mem_get_info(dev)[0]
+    return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
 
 
 def _prior_entries_finite(a, b):

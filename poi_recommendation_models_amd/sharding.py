@@ -45,15 +45,14 @@ def broadcast_module(model, src=0, group=None):
 
 def gather_topk(local_users, local_ids, local_scores, num_users, group=None):
     """All-gather per-rank [n_r, k] top-k blocks and return (ids, scores) as [num_users, k]
-    tensors in user order, on every rank. Blocks are padded to the largest n_r."""
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
+    tensors in user order, on every rank. Blocks are padded to the largest n_r. Every exchange is
+    one all_gather_into_tensor into a [world * m, ...] buffer: the call RCCL runs, and the one the
+    gloo tests run."""
+    world = _world(group)
     dev = local_ids.device
     k = local_ids.shape[1]
     n = torch.tensor([len(local_users)], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    ns = [int(x.item()) for x in ns]
+    ns = all_gather_cat(n, group).tolist()
     m = max(ns) if ns else 0
     pad_u = torch.full((m,), -1, dtype=torch.int64, device=dev)
     pad_u[:len(local_users)] = torch.as_tensor(np.asarray(local_users, dtype=np.int64), device=dev)
@@ -61,12 +60,9 @@ def gather_topk(local_users, local_ids, local_scores, num_users, group=None):
     pad_i[:len(local_users)] = local_ids.to(torch.int64)
     pad_s = torch.full((m, k), float("nan"), dtype=torch.float32, device=dev)
     pad_s[:len(local_users)] = local_scores
-    gu = [torch.empty_like(pad_u) for _ in range(world)]
-    gi = [torch.empty_like(pad_i) for _ in range(world)]
-    gs = [torch.empty_like(pad_s) for _ in range(world)]
-    dist.all_gather(gu, pad_u, group=group)
-    dist.all_gather(gi, pad_i, group=group)
-    dist.all_gather(gs, pad_s, group=group)
+    gu = all_gather_cat(pad_u, group).view(world, m)
+    gi = all_gather_cat(pad_i, group).view(world, m, k)
+    gs = all_gather_cat(pad_s, group).view(world, m, k)
     ids = torch.full((num_users, k), -1, dtype=torch.int64, device=dev)
     sc = torch.full((num_users, k), float("nan"), dtype=torch.float32, device=dev)
     for r in range(world):
@@ -74,6 +70,23 @@ def gather_topk(local_users, local_ids, local_scores, num_users, group=None):
         ids[u] = gi[r][:ns[r]]
         sc[u] = gs[r][:ns[r]]
     return ids, sc
+
+
+def _world(group=None):
+    import torch.distributed as dist
+    return dist.get_world_size(group)
+
+
+def all_gather_cat(block, group=None):
+    """[world * block.shape[0], ...] <- every rank's `block` in rank order, by ONE
+    all_gather_into_tensor (RCCL: a ring over xGMI; gloo accepts the same concatenated form, so
+    the CPU tests execute the call the GPUs run)."""
+    import torch.distributed as dist
+    block = block.contiguous()
+    out = torch.empty((_world(group) * block.shape[0], *block.shape[1:]), dtype=block.dtype,
+                      device=block.device)
+    dist.all_gather_into_tensor(out, block, group=group)
+    return out
 
 
 def column_blocks(num_pois, world):
@@ -134,6 +147,9 @@ def distributed_plan(csr, num_users, num_pois, k, world, model=None):
     return "users"
 
 
+MERGE_F64_CAP = 2048    # candidates per row of nais_topk_merge_f64 (include/nais.h)
+
+
 def distributed_topk(model, train_matrix, num_users, k, group=None, **kw):
     """[num_users, k] (ids, scores) of users 0..num_users-1 computed by all ranks of `group`, the
     same on every rank: column-sharded pairs route or user-sharded per-user kernels
@@ -144,8 +160,10 @@ def distributed_topk(model, train_matrix, num_users, k, group=None, **kw):
     model.eval()
     csr = device_csr(train_matrix, model._check_device())
     P = model._item_tables()[0].shape[0]
+    prior = kw.get("prior") is not None
+    # the prior's f64 merge (nais_topk_merge_f64) holds at most MERGE_F64_CAP candidates per user
     if distributed_plan(csr, num_users, P, k, world, model) == "pairs" and not (
-            kw.get("prior") is not None and model._pairs_only):
+            prior and (model._pairs_only or world * k > MERGE_F64_CAP)):
         return distributed_topk_pairs(model, csr, range(num_users), k, group=group, **kw)
     mine = shard_users(csr.hist_len[:num_users], P, world)[rank]
     ids, sc = score_topk(model, csr, mine, k, **kw)
@@ -194,32 +212,43 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
                          "(use the user-sharded path, distributed_topk falls back to it)")
     c0, c1 = column_blocks(P, world)[rank]
     prior = kw.get("prior")
-    if prior is not None:
-        ids, sc, keys = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
-                                          kw.get("latlon_mat"), None, force=True, cols=(c0, c1),
-                                          events=events, prior=prior,
-                                          group=(group if group is not None else dist.group.WORLD)
-                                          if world > 1 else None, return_keys=True)
-        if world == 1:
-            return ids, sc
-        gi = torch.empty(world, n, k, dtype=torch.int64, device=dev)
-        gk = torch.empty(world, n, k, dtype=torch.float64, device=dev)
-        _all_gather_blocks(gi, ids, group)
-        _all_gather_blocks(gk, keys, group)
-        return merge_topk_f64(gi, gk, k)
-    ids, sc = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
-                                kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events)
+    if n == 0:
+        z = torch.empty(0, k, dtype=torch.int64, device=dev)
+        return z, torch.empty(0, k, dtype=torch.float32, device=dev)
+    grp = (group if group is not None else dist.group.WORLD) if world > 1 else None
+    out = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
+                            kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events,
+                            prior=prior, group=grp if prior is not None else None,
+                            return_keys=prior is not None)
     if world == 1:
-        return ids, sc
-    gi = torch.empty(world, n, k, dtype=torch.int64, device=dev)
-    gs = torch.empty(world, n, k, dtype=torch.float32, device=dev)
-    if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(gi.unbind(0)), ids.contiguous(), group=group)
-        dist.all_gather(list(gs.unbind(0)), sc.contiguous(), group=group)
-    else:
-        dist.all_gather_into_tensor(gi, ids.contiguous(), group=group)
-        dist.all_gather_into_tensor(gs, sc.contiguous(), group=group)
-    return merge_topk(gi, gs, k)
+        return out[0], out[1]
+    ids, sc = out[0], out[1]
+    # the exchange: one all-gather of this rank's [n, k] block per array ([world * n, k], rank
+    # order = ascending POI ranges), then the merge over the world * k candidates per user
+    mark = _marker(events, dev)
+    gi = all_gather_cat(ids, group).view(world, n, k)
+    gk = all_gather_cat(out[2] if prior is not None else sc, group).view(world, n, k)
+    mark("allgather")
+    res = merge_topk_f64(gi, gk, k) if prior is not None else merge_topk(gi, gk, k)
+    mark("merge")
+    return res
+
+
+def _marker(events, dev):
+    """mark(kind): records a (kind, start, end) event pair on the current stream covering the work
+    issued since the previous mark (bench.py's per-phase times); a no-op without `events`."""
+    if events is None:
+        return lambda kind: None
+    stream = torch.cuda.current_stream(dev)
+    last = [torch.cuda.Event(enable_timing=True)]
+    last[0].record(stream)
+
+    def mark(kind):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(stream)
+        events.append((kind, last[0], e, 1))
+        last[0] = e
+    return mark
 
 
 def agree_min(value, device, group=None):
@@ -238,15 +267,6 @@ def allreduce_gmax(gmax_bits, group=None):
     import torch.distributed as dist
     dist.all_reduce(gmax_bits, op=dist.ReduceOp.MAX, group=group)
     return gmax_bits
-
-
-def _all_gather_blocks(out, block, group):
-    """out[world, ...] <- every rank's `block` (gloo: list all_gather; RCCL: one tensor)."""
-    import torch.distributed as dist
-    if dist.get_backend(group) == "gloo":
-        dist.all_gather(list(out.unbind(0)), block.contiguous(), group=group)
-    else:
-        dist.all_gather_into_tensor(out, block.contiguous(), group=group)
 
 
 def merge_topk_f64(ids, keys, k):
@@ -292,12 +312,7 @@ def allgather_rows(local_rows, num_rows, group=None):
     d = local_rows.shape[1]
     block = torch.zeros(S, d, dtype=local_rows.dtype, device=local_rows.device)
     block[:local_rows.shape[0]] = local_rows
-    full = torch.empty(S * world, d, dtype=local_rows.dtype, device=local_rows.device)
-    if hasattr(dist, "all_gather_into_tensor") and dist.get_backend(group) != "gloo":
-        dist.all_gather_into_tensor(full, block, group=group)
-    else:
-        dist.all_gather(list(full.chunk(world)), block, group=group)
-    return full[:num_rows]
+    return all_gather_cat(block, group)[:num_rows]
 
 
 def row_block(num_rows, rank, world):

@@ -33,9 +33,17 @@ def _distributed_world():
 
 
 def _want_distributed(distributed):
-    """distributed=None reads NAIS_DISTRIBUTED_EVAL; True requires a group of > 1 rank."""
-    if distributed is None:
-        distributed = os.environ.get("NAIS_DISTRIBUTED_EVAL", "0") == "1"
+    """distributed=None reads NAIS_DISTRIBUTED_EVAL (falls back to one process, with a warning,
+    when no group of > 1 rank exists); distributed=True requires such a group."""
+    if distributed is None:     # the env opt-in: single-process when there is no group to use
+        if os.environ.get("NAIS_DISTRIBUTED_EVAL", "0") != "1":
+            return False
+        if _distributed_world() <= 1:
+            import warnings
+            warnings.warn("NAIS_DISTRIBUTED_EVAL=1 without a process group of > 1 rank: "
+                          "evaluating in this process")
+            return False
+        return True
     if not distributed:
         return False
     if _distributed_world() <= 1:

@@ -17,6 +17,8 @@ def _data(kind):
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
     if kind == "shared":          # 200 users x U{1..80} items over 2,000 POIs: sharing ~4
         data = make_checkins(200, 2000, 80, seed=21)
+    elif kind == "shared_odd":    # 1,002 POIs: two column shards of 501, narrower than a table
+        data = make_checkins(200, 1002, 80, seed=21)    # block and odd (pitch rounded up to 504)
     else:                         # 12 users, little overlap: sharing ~1
         data = make_checkins(12, 3000, 30, seed=22)
     p = init_nais_params(data.num_pois, 32, 32, seed=23, emb_std=0.3, bias_std=0.1)
@@ -53,7 +55,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("kind,plan", [("shared", "pairs"), ("sparse", "users")])
+@pytest.mark.parametrize("kind,plan", [("shared", "pairs"), ("shared_odd", "pairs"), ("sparse", "users")])
 def test_distributed_topk_two_ranks_equal_single(kind, plan):
     import torch.multiprocessing as mp
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
@@ -120,13 +122,13 @@ def test_validation_autoroute_two_ranks_equal_single(kind):
         np.testing.assert_array_equal(r, ref)
 
 
-def _worker_prior(rank, world, port, out):
+def _worker_prior(rank, world, port, out, kind="shared"):
     import torch.distributed as dist
     from poi_recommendation_models_amd import sharding
     from poi_recommendation_models_amd.catalog import DeviceCSR
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    data, p = _data("shared")
+    data, p = _data(kind)
     m = _model(p, data.num_pois)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, data.num_pois, torch.device("cuda:0"))
     plan = sharding.distributed_plan(csr, data.num_users, data.num_pois, 50, world, m)
@@ -137,7 +139,8 @@ def _worker_prior(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_distributed_prior_column_shards_equal_single():
+@pytest.mark.parametrize("kind", ["shared", "shared_odd"])
+def test_distributed_prior_column_shards_equal_single(kind):
     """the power-law prior no longer drops to user sharding at N > 1: two ranks
     own half the POI columns each, normalise by the all-reduced max G and merge on the f64 blended
     score -- ids and scores identical to the single-process blend of the pairs route."""
@@ -145,10 +148,10 @@ def test_distributed_prior_column_shards_equal_single():
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "p")
-        mp.start_processes(_worker_prior, args=(2, _free_port(), out), nprocs=2, join=True,
+        mp.start_processes(_worker_prior, args=(2, _free_port(), out, kind), nprocs=2, join=True,
                            start_method="spawn")
         res = [np.load(f"{out}_{r}.npz") for r in range(2)]
-    data, p = _data("shared")
+    data, p = _data(kind)
     m = _model(p, data.num_pois)
     csr = DeviceCSR.from_arrays(data.indptr, data.indices, data.num_pois, torch.device("cuda:0"))
     prior = (0.052, -1.37, 0.2, data.place_coords)

@@ -166,6 +166,26 @@ def test_catalog_golden_fp16x3_pairsplit(variant, strategy):
     test_catalog_golden(variant, "trained", "fp16x3_pairsplit", strategy)
 
 
+# users the metrics tests may excuse (a reference tie run within TIE_ULPS straddling some k of
+# k_list, read from the fixture's own scores): none of the four golden fixtures has one, so the
+# 6-tuples must equal the reference's exactly
+MAX_EXCUSED_USERS = 0
+
+
+def _metrics_exact(got, z, rec, ks):
+    """the 6-tuple exactly equal to the reference's (tests/_helpers.py
+    assert_metrics_exact); prints and bounds the users a straddling tie run excuses."""
+    from _helpers import assert_metrics_exact
+    excused = assert_metrics_exact(got, z["trained/topk_ids"], z["trained/topk_scores"], rec,
+                                   positives_from(z, "val"), positives_from(z, "test"), ks,
+                                   tie_ulps=TIE_ULPS)
+    users = sorted({u for u, _ in excused})
+    print(f"metrics: {len(users)} user(s) excused by a tie run straddling k: {excused}")
+    assert len(users) <= MAX_EXCUSED_USERS, excused
+    if not excused:
+        np.testing.assert_array_equal(np.array(got), z["trained/metrics"])
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_validation_dropin_metrics(precision):
     """validation.NAIS_validation returns the reference's 6-tuple on the golden dataset."""
@@ -180,13 +200,8 @@ def test_validation_dropin_metrics(precision):
         topk = 50
     got = V.NAIS_validation(m, Args(), U, positives_from(z, "test"), positives_from(z, "val"), X,
                             [5, 10, 15, 20, 25, 30])
-    ref = z["trained/metrics"]
-    # identical unless a tie run straddles a cut-off k; then recompute on our own lists
     rec = V.recommend(m, Args(), U, X)
-    mine = metrics_oracle.evaluate(positives_from(z, "val"), rec, [5, 10, 15, 20, 25, 30]) + \
-        metrics_oracle.evaluate(positives_from(z, "test"), rec, [5, 10, 15, 20, 25, 30])
-    np.testing.assert_array_equal(np.array(got), np.array(mine))
-    np.testing.assert_allclose(np.array(got), ref, atol=2.0 / U)
+    _metrics_exact(got, z, rec, [5, 10, 15, 20, 25, 30])
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
@@ -206,10 +221,7 @@ def test_region_validation_dropin_metrics(precision):
     got = V.NAIS_region_validation(m, Args(), U, positives_from(z, "test"), positives_from(z, "val"),
                                    X, z["region_of"], ks)
     rec = V.recommend(m, Args(), U, X, region_of=z["region_of"])
-    mine = metrics_oracle.evaluate(positives_from(z, "val"), rec, ks) + \
-        metrics_oracle.evaluate(positives_from(z, "test"), rec, ks)
-    np.testing.assert_array_equal(np.array(got), np.array(mine))
-    np.testing.assert_allclose(np.array(got), z["trained/metrics"], atol=2.0 / U)
+    _metrics_exact(got, z, rec, ks)
 
 
 # ------------------------------------------------------------ seeded oracle parity, many shapes
@@ -285,7 +297,8 @@ def test_distance_validation_dropin():
     got = V.NAIS_region_distance_validation(m, Args(), U, positives_from(z, "test"),
                                             positives_from(z, "val"), X, z["region_of"], None,
                                             [5, 10, 15, 20, 25, 30], poi_coords=z["coords"])
-    np.testing.assert_allclose(np.array(got), z["trained/metrics"], atol=2.0 / U)
+    rec = V.recommend(m, Args(), U, X, region_of=z["region_of"], coords=z["coords"])
+    _metrics_exact(got, z, rec, [5, 10, 15, 20, 25, 30])
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

@@ -278,3 +278,20 @@ def test_train_oracle_region_variants_match_reference(case):
     for k, g in r["grads"].items():
         ref = z[pre + "grad/" + k]
         assert np.max(np.abs(g.reshape(ref.shape) - ref)) <= 2e-6 * np.abs(ref).max(), k
+
+
+def test_metric_fixtures_have_no_straddling_ties():
+    """The GPU metrics tests (test_gpu_parity.py::_metrics_exact) demand the reference's 6-tuple
+    exactly unless a tie run straddles a cut-off k: pin that the golden fixtures hold none, and
+    that the 6-tuple restated from the reference's own top-k lists is the captured one."""
+    from _helpers import positives_from, straddles
+    from oracle import metrics_oracle
+    ks = [5, 10, 15, 20, 25, 30]
+    for f in ("catalog_basic", "catalog_region", "catalog_distance", "catalog_region_distance"):
+        z = load_golden(f + ".npz")
+        sc = z["trained/topk_scores"]
+        assert not any(straddles(sc[u], k, 4) for u in range(len(sc)) for k in ks), f
+        rid = z["trained/topk_ids"].tolist()
+        m = metrics_oracle.evaluate(positives_from(z, "val"), rid, ks) + \
+            metrics_oracle.evaluate(positives_from(z, "test"), rid, ks)
+        np.testing.assert_array_equal(np.array(m), z["trained/metrics"])
