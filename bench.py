@@ -40,7 +40,6 @@ PRODUCTS = {"fp32": 1, "fp16x3": 3, "fp16x3_pairsplit": 3, "fp16x6": 6, "fp16x6_
 PEAKS = {k: (PEAK_FP32_MFMA_TFLOPS if v == 1 else PEAK_F16_MFMA_TFLOPS / v) for k, v in PRODUCTS.items()}
 HBM_SPEC_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
 HBM_MEASURED_GBS = 6290.0      # MI355X_MICROARCH.md: float4 copy, measured
-L2_PEAK_GBS = 34500.0          # MI355X_MICROARCH.md: L2 aggregate (8 XCDs), measured
 DTYPES = {
     "fp32": "fp32 (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulate)",
     "fp16x6": "fp32-faithful: W1 x products as 6 f16 MFMA products of exact hi/mid/lo fp16 splits "
@@ -790,8 +789,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     entries = int(hist_len.sum())
     J = int(np.count_nonzero(np.bincount(data.indices, minlength=P)))
     fused = catalog.PAIR_FUSED_TOPK and K <= 256
-    l2 = fused and catalog.PAIR_L2_GATHER
-    Wb, st_w = catalog.PAIR_BLOCK_COLS, (64 if l2 else catalog.PAIR_STRIPE)
+    Wb, st_w = catalog.PAIR_BLOCK_COLS, catalog.PAIR_STRIPE
     stripes = sum((min(Wb, NC - b) + st_w - 1) // st_w for b in range(0, NC, Wb))
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -801,10 +799,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B
         # per entry) + score rows (4 B per user x column; the fused kernel writes only the top-k
         # merges); with PAIR_TABLE_GATHER_FRAC > 0 only the gather stream's share is timed
-        # (L2 route: a launch = one 64-column chunk; + 12 B per user for its k-th key and count)
         gbytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
-        if l2:
-            gbytes += a.num_users * 12 * stripes
         gbytes *= per.get("gather_share", 1.0)
         g_ms = sum(per.get("gather", [])) / a_steps[precision]
         t_ms = sum(per.get("table", [])) / a_steps[precision]
@@ -815,23 +810,15 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         t_ach = tflops / (t_ms * 1e-3) / 1e12 if t_ms else None
         gcus = ncu - table_cus if table_cus < ncu else ncu
         gather = {
-            "kernel": ("pair_gather_topk_l2_kernel (nais_pair_gather_topk_l2)" if l2 else
-                       "pair_gather_topk_kernel (nais_pair_gather_topk)") if fused else
+            "kernel": "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
                       "pair_gather_kernel (nais_pair_gather)",
             "bound": "hbm", "achieved": g_ach, "peak": HBM_SPEC_GBS, "unit": "GB/s",
             "frac": g_ach / HBM_SPEC_GBS if g_ach else None,
             "frac_of_measured_hbm": g_ach / HBM_MEASURED_GBS if g_ach else None,
             "measured_hbm_peak": HBM_MEASURED_GBS,
-            "served_from": ("the XCDs' L2 mostly: all waves walk each 64-column chunk's table in "
-                            "blocks of %d rows (x 512 B), so a block's rows stay in L2 while every "
-                            "user adds its entries from it; L2 peak %.1f TB/s chip-wide, %.1f TB/s "
-                            "for these %d CUs" % (catalog.PAIR_L2_ROWS, L2_PEAK_GBS / 1e3,
-                                                   L2_PEAK_GBS * gcus / ncu / 1e3, gcus)) if l2 else
-                          ("Infinity Cache (MALL) mostly: the 256-column stripe of the tables "
-                           "(J x 256 x 8 B ~ 205 MB) fits the 256 MB MALL, so the memory side "
-                           "delivers more than the HBM copy rate"),
-            "frac_of_l2_peak_for_its_cus": (g_ach / (L2_PEAK_GBS * gcus / ncu) if g_ach else None) if l2
-                                           else None,
+            "served_from": ("Infinity Cache (MALL) mostly: the 256-column stripe of the tables "
+                            "(J x 256 x 8 B ~ 205 MB) fits the 256 MB MALL, so the memory side "
+                            "delivers more than the HBM copy rate"),
             "algorithmic_bytes_per_launch": gbytes / n_gl, "avg_launch_ms": g_ms / n_gl,
             "launches_per_step": n_gl, "ms_per_step": g_ms, "cus": gcus,
         }
@@ -857,8 +844,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     other = gather if dominant is table else table
     try:
         tj = json.load(open(a.traffic_json))
-        key = (("pairs_gather_topk_l2" if l2 else "pairs_gather_topk") if fused else "pairs_gather") \
-            if dominant is gather else \
+        key = ("pairs_gather_topk" if fused else "pairs_gather") if dominant is gather else \
             "pairs_table_" + a.precision
         e = tj.get(key, {})
         ok = (e.get("num_users") == a.num_users and e.get("num_pois") == P and e.get("world") == world
@@ -871,10 +857,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         dominant["traffic"] = None
     if "traffic" not in dominant:
         dominant["traffic"] = None
-    dominant["note"] = ("gather: algorithmic bytes per launch (one %d-column %s) = sum_u h_u x "
-                        "columns x 8 B table reads + 12 B CSR id + row map per history entry%s; table: "
-                        % (st_w, "chunk" if l2 else "stripe", " + 12 B k-th key and count per user"
-                           if l2 else "") +
+    dominant["note"] = ("gather: algorithmic bytes per launch (one %d-column stripe) = sum_u h_u x "
+                        "columns x 8 B table reads + 12 B CSR id + row map per history entry; table: "
+                        % st_w +
                         "SURVEY.md 8(d) FLOP per (pair, history item) x distinct history POIs x "
                         "columns; traffic = rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per launch")
     dominant["overlap"] = ("tables on CUs [0, %d) and gathers on the other %d, side by side on "

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 7
+#define NAIS_ABI_VERSION 8
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -226,22 +226,6 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *                      be any block; the calls of one user list must be stream-ordered. k <= 256.
  *   nais_topk_keys_finish  keys -> out_ids / out_scores [num_users, k] (short lists padded with
  *                      -1 / NaN and counted into *short_count), as nais_topk_rows reports them.
- *
- * L2-blocked form of the fused route (an A/B knob, off by default -- 2-3x slower than
- * nais_pair_gather_topk so far; DESIGN.md "L2-blocked gather"):
- *   nais_pair_table_il the same pair terms as nais_pair_table in ONE interleaved, chunk-major
- *                      table: (e, es) of (row r, column c) at
- *                      table[((c-col0)/64)*chunk_stride + r*128 + ((c-col0)%64)*2];
- *                      chunk_stride >= num_items * 128 floats, and even (float2 loads).
- *   nais_pair_gather_topk_l2  nais_pair_gather_topk over such a table (num_rows = num_items):
- *                      one launch per 64-column chunk; each wave keeps up to 32 users' sums in
- *                      registers and walks the table in blocks of rows_per_block rows (a block's
- *                      rows stay in the XCD's L2 while every user adds its entries from it).
- *                      max_waves = the waves the gather's CUs hold at once (users per wave =
- *                      ceil(num_users / max_waves), <= 32). Requires each user's CSR row sorted by
- *                      POI id (scipy's canonical CSR, the reference's tocsr(), datasets.py:262);
- *                      then the sums run in CSR order and the result equals
- *                      nais_pair_gather_topk's bit for bit. k <= 256.
  */
 size_t nais_pair_rows_workspace_size(int64_t num_pois);
 int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int32_t* users,
@@ -305,16 +289,6 @@ int32_t nais_topk_blend_rows_f64(const float* scores, int64_t score_ld, const do
 int32_t nais_topk_merge_f64(const double* keys, const int64_t* ids, int32_t num_rows, int32_t m,
                             int32_t k, int64_t* out_ids, float* out_scores, double* out_keys,
                             void* stream);
-int32_t nais_pair_table_il(const nais_params_t* params, const int64_t* items, int64_t num_items,
-                           int64_t col0, int64_t cols, const int64_t* region_of,
-                           const double* coords, const double* latlon_mat, float* table,
-                           int64_t chunk_stride, void* stream);
-int32_t nais_pair_gather_topk_l2(const float* table, int64_t chunk_stride, int64_t num_rows,
-                                 const int32_t* rowmap, const int64_t* indptr, const int64_t* indices,
-                                 const int32_t* users, int32_t num_users, int64_t col0, int64_t cols,
-                                 float beta, int32_t k, uint64_t* keys, int32_t* kcount,
-                                 int32_t* nan_count, int32_t rows_per_block, int32_t max_waves,
-                                 void* stream);
 
 /*
  * A stream restricted to the CUs whose bits are set in cu_mask[mask_words] (bit i = CU i), for

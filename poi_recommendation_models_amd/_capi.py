@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
@@ -30,7 +30,7 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_linear_rows", "nais_dot_forward", "nais_dot_pair_table", "nais_dot_single_fixup",
            "nais_disent_forward", "nais_pair_distances", "nais_train_forward_ex",
            "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
-           "nais_pair_table_il", "nais_pair_gather_topk_l2", "nais_pair_prior_table",
+           "nais_pair_prior_table",
            "nais_pair_prior_gather", "nais_topk_blend_rows", "nais_topk_blend_rows_f64",
            "nais_topk_merge_f64", "nais_train_ucache_size")
 
@@ -199,12 +199,6 @@ def load(path: str | None = None):
     lib.nais_pair_gather_topk.restype = i32
     lib.nais_pair_gather_topk.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp,
                                           vp]
-    lib.nais_pair_table_il.restype = i32
-    lib.nais_pair_table_il.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp,
-                                       i64, vp]
-    lib.nais_pair_gather_topk_l2.restype = i32
-    lib.nais_pair_gather_topk_l2.argtypes = [vp, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp,
-                                             vp, vp, i32, i32, vp]
     lib.nais_pair_prior_table.restype = i32
     lib.nais_pair_prior_table.argtypes = [vp, i64, vp, i64, i64, i64, f64, f64, vp, i64, vp]
     lib.nais_pair_prior_gather.restype = i32

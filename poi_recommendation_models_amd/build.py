@@ -13,10 +13,10 @@ OUT = os.path.join(HERE, "libnais_hip.so")
 ARCH = os.environ.get("NAIS_OFFLOAD_ARCH", "gfx950")
 
 
-# nais_kernels.hip: MFMAs in their VGPR form (accumulators in VGPRs, not AGPRs). The one-wave-per-
-# SIMD pair-table kernel (pair_table_x3c_kernel, 256 + AGPRs) otherwise gets AGPR accumulators and
-# pays a v_accvgpr_read per epilogue value; every other kernel of the file compiles identically
-# either way (same VGPR / AGPR counts).
+# nais_kernels.hip: MFMAs in their VGPR form (accumulators in VGPRs, not AGPRs), so an epilogue
+# reads its accumulator values without a v_accvgpr_read each. (Introduced for the round-3 x3c
+# pair-table A/B, since removed; the remaining kernels compiled to the same VGPR / AGPR counts
+# either way.)
 PER_SRC = {"nais_kernels.hip": ("-mllvm", "-amdgpu-mfma-vgpr-form=1")}
 
 

@@ -252,17 +252,10 @@ PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 # 542.6 / 552.6 / 614.8 ms while the gather stream's own time fell only 539 -> 532 ms
 # (profiles/r1/table_gather_frac/; results bit-identical, test_pairs_blocks_passes_bit_identical).
 PAIR_TABLE_GATHER_FRAC = 0.0
-# L2-blocked fused gather (nais_pair_gather_topk_l2 over one interleaved chunk-major table): each
-# wave keeps up to 32 users' sums of a 64-column chunk in registers while all waves walk the table
-# in blocks of PAIR_L2_ROWS rows (~1.5 MB), so the rows shared by ~50 users come from the XCD's L2
-# rather than the Infinity Cache. Same sums in the same order as nais_pair_gather_topk.
 # Table launches alternate over two streams with the same CU mask, so block b + 1's workgroups
 # fill the CUs that block b's last, partial round of workgroups leaves idle (1,564 workgroups of
 # one table block = 9.8 rounds over 160 CUs; one stream waits for the whole launch to drain).
 PAIR_TABLE_STREAMS = int(os.environ.get("NAIS_PAIR_TABLE_STREAMS", "2"))
-PAIR_L2_GATHER = os.environ.get("NAIS_PAIR_L2", "0") == "1"   # A/B knob, off: 2-3x slower
-PAIR_L2_ROWS = int(os.environ.get("NAIS_PAIR_L2_ROWS", "3072"))
-PAIR_L2_WAVES_PER_CU = int(os.environ.get("NAIS_PAIR_L2_WAVES_PER_CU", "20"))
 _masked: dict = {}
 
 
@@ -422,17 +415,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
         prior_flags = _capi.PRIOR_FINITE if _prior_entries_finite(pa, pb) else 0
     pr_of = {}   # column-block table -> its float64 pr_d table (prior only)
-    # the L2-blocked gather reads the interleaved table that nais_pair_table_il writes (the NAIS
-    # catalog kernels; other cores keep the two row-major tables)
-    l2 = fused and PAIR_L2_GATHER and type(model)._pair_table is _NAISDevice._pair_table
 
     def table(tab, c0, w, stream_):
-        if l2:
-            model._pair_table_il(lib, prm, items, J, c0, w, reg, cor, llm, tab.data_ptr(), J * 128,
-                                 stream_)
-        else:
-            model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
-                              tab[1].data_ptr(), ld, stream_)
+        model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
+                          tab[1].data_ptr(), ld, stream_)
         if prior is not None:
             _capi.check(lib.nais_pair_prior_table(pri_coords.data_ptr(), P, items.data_ptr(), J, c0, w,
                                                   float(pa), float(pb), pr_of[id(tab)].data_ptr(), ld,
@@ -458,8 +444,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
-        def gather_launches(w):   # one fused-gather kernel per 256-column stripe / 64-column chunk
-            return (w + (64 if l2 else PAIR_STRIPE) - 1) // (64 if l2 else PAIR_STRIPE) if fused else 1
+        def gather_launches(w):   # one fused-gather kernel per 256-column stripe
+            return (w + PAIR_STRIPE - 1) // PAIR_STRIPE if fused else 1
         if fused:
             keys = torch.empty(m, k, dtype=torch.int64, device=dev)
             kcount = torch.zeros(m, dtype=torch.int32, device=dev)
@@ -467,13 +453,6 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             def gather(tab, c0, w, stream_, a=0, b=None):   # launch slots [a, b) of u_dev
                 b = m if b is None else b
                 if b <= a:
-                    return
-                if l2:
-                    _capi.check(lib.nais_pair_gather_topk_l2(
-                        tab.data_ptr(), J * 128, J, rowmap.data_ptr(), csr.indptr.data_ptr(),
-                        csr.indices.data_ptr(), u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta),
-                        k, keys.data_ptr() + 8 * k * a, kcount.data_ptr() + 4 * a, counters[0:1].data_ptr(),
-                        PAIR_L2_ROWS, gather_waves, stream_), "nais_pair_gather_topk_l2")
                     return
                 _capi.check(lib.nais_pair_gather_topk(
                     tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
@@ -512,9 +491,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 events.append(("block_cols", None, None, W))
             overlap = (0 < table_cus < ncu and len(blocks) > 1 and stream is None
                        and not no_side_streams)
-            gather_waves = (ncu - table_cus if overlap else ncu) * PAIR_L2_WAVES_PER_CU
-            shape = ((W + 63) // 64, J, 128) if l2 else (2, J, ld)
-            tabs = [torch.empty(*shape, dtype=torch.float32, device=dev)
+            tabs = [torch.empty(2, J, ld, dtype=torch.float32, device=dev)
                     for _ in range(2 if overlap else 1)]
             if prior is not None:
                 pr_of.update({id(t): torch.empty(J, ld, dtype=torch.float64, device=dev) for t in tabs})

@@ -37,41 +37,14 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-#ifndef NAIS_WAVES
-#define NAIS_WAVES 8
-#endif
-#ifndef NAIS_X3B_NW
-#define NAIS_X3B_NW NAIS_WAVES   // waves per workgroup of the item-side split kernel
-#endif
-#ifndef NAIS_X3B_DIST
-#define NAIS_X3B_DIST 1   // distance variants on the item-side kernel where it pipelines (D, H <= 64)
-#endif
-#ifndef NAIS_X3B_SCHED
-#define NAIS_X3B_SCHED 0
-#endif
-#ifndef NAIS_X3B_WIDE
-// 1 (default): the item-side split kernel also for D or H > 64, at 8 waves (2 per SIMD) with one
-// accumulator pass of two hidden blocks at a time and b1 / w2 read from LDS (config 5: direct
-// 369 -> 387 TF, pair tables 319 -> 323 TF on 224 CUs; profiles/r1/cfg5_wide8/). 0: the per-pair
-// split kernel there. (An earlier 4-wave / 512-VGPR form was slower: 285 TF direct.)
-#define NAIS_X3B_WIDE 1
-#endif
-#ifndef NAIS_X3B_WIDE_ILV
-// 1: wide shapes build the next group's A_j item by item between this group's MFMA chains
-// instead of all at once before them (A/B; 0 = default)
-#define NAIS_X3B_WIDE_ILV 0
-#endif
-constexpr int WAVES = NAIS_WAVES;           // 512-thread workgroups
+constexpr int WAVES = 8;                    // 512-thread workgroups (2 waves per SIMD)
 constexpr int THREADS = WAVES * 64;
 constexpr int CAND_PER_BLOCK = WAVES * 32;  // one 32-candidate MFMA column tile per wave
 constexpr int JC = 64;                      // history rows staged in LDS per chunk
 constexpr int TOPK_THREADS = 1024;
 constexpr int MAX_K = 1024;
 constexpr int MAX_BATCH_USERS = 512;        // users scored per catalog launch
-#ifndef NAIS_PAIR_GROUP_ITEMS
-#define NAIS_PAIR_GROUP_ITEMS 128
-#endif
-constexpr int PAIR_GROUP_ITEMS = NAIS_PAIR_GROUP_ITEMS;   // item rows per workgroup in pair-table mode
+constexpr int PAIR_GROUP_ITEMS = 128;       // item rows per workgroup in pair-table mode
 
 struct DevParams {
   const float* eh;
@@ -93,52 +66,31 @@ struct DevParams {
 //   e = exp(a) * [item != c]  to e[r * ld + c - col0]   and   e * (h . t)  to es[...]
 // -- all a user needs from the pair: pair_gather_kernel sums them over each user's history rows.
 // e == nullptr: the normal per-user scoring.
-#ifndef NAIS_TABLE_NT
-#define NAIS_TABLE_NT 0
-#endif
-// pair-table stores (A/B knob: non-temporal, so the tables streaming out do not evict the
-// gather's stripe from the Infinity Cache)
-__device__ __forceinline__ void tab_store(float* p, float v) {
-  if (NAIS_TABLE_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
 struct TableOut {
   float* e = nullptr;
   float* es = nullptr;
   int64_t ld = 0, col0 = 0, cols = 0, nitems = 0;
   int32_t gi = 0;
-  // cs > 0: one interleaved, chunk-major table instead of two row-major ones (the L2-blocked
-  // gather's layout): (e, es) of (row r, column offset x) at e[(x / 64) * cs + r * 128 + (x % 64) * 2]
-  int64_t cs = 0;
 };
 // the pair's two terms for item row `row` (relative to the launch's base) and column offset x
 __device__ __forceinline__ void tab_put(const TableOut& t, int64_t row, int64_t x, float e, float es) {
-  if (t.cs) {
-    *reinterpret_cast<float2*>(t.e + (x >> 6) * t.cs + row * 128 + (x & 63) * 2) = make_float2(e, es);
-  } else {
-    const int64_t o = row * t.ld + x;
-    tab_store(t.e + o, e);
-    tab_store(t.es + o, es);
-  }
+  const int64_t o = row * t.ld + x;
+  t.e[o] = e;
+  t.es[o] = es;
 }
 
-#ifndef NAIS_TILE_MAJOR
-#define NAIS_TILE_MAJOR 0
-#endif
-// Catalog grid: one workgroup per (user slot, 256-POI tile). Default user-major dispatch order
-// (blockIdx.x = tile): a user's ~400 workgroups run back to back, heaviest users first.
-// NAIS_TILE_MAJOR=1 swaps the order so that workgroups reading the same 64 KB of target rows
-// share an XCD's L2 (fabric traffic 6.7 GB -> ~0.2 GB per 256-user launch) -- measured slower
-// (fp32 -11 %, fp16x3 -3 %, profiles/r1/ab_tilemajor.json): the kernel is MFMA-bound and the
-// Infinity Cache serves the re-reads at ~40 GB/s, far below any limit.
-__device__ __forceinline__ int cat_user_slot() { return NAIS_TILE_MAJOR ? blockIdx.x : blockIdx.y; }
-__device__ __forceinline__ int cat_tile() { return NAIS_TILE_MAJOR ? blockIdx.y : blockIdx.x; }
+// Catalog grid: one workgroup per (user slot, 256-POI tile), user-major dispatch order
+// (blockIdx.x = tile): a user's ~400 workgroups run back to back, heaviest users first. (A
+// tile-major order that keeps the 64 KB of target rows per tile in one XCD's L2 measured slower:
+// fp32 -11 %, fp16x3 -3 %, profiles/r1/ab_tilemajor.json -- the kernel is MFMA-bound and the
+// Infinity Cache serves the re-reads far below any limit.)
+__device__ __forceinline__ int cat_user_slot() { return blockIdx.y; }
+__device__ __forceinline__ int cat_tile() { return blockIdx.x; }
 inline dim3 table_grid(const TableOut& t, int ngroups, int cand_per_block = CAND_PER_BLOCK) {
   return dim3((unsigned)((t.cols + cand_per_block - 1) / cand_per_block), (unsigned)ngroups);
 }
 inline dim3 cat_grid(int64_t P, int nb, int cand_per_block) {
-  const unsigned tiles = (unsigned)((P + cand_per_block - 1) / cand_per_block);
-  return NAIS_TILE_MAJOR ? dim3((unsigned)nb, tiles) : dim3(tiles, (unsigned)nb);
+  return dim3((unsigned)((P + cand_per_block - 1) / cand_per_block), (unsigned)nb);
 }
 
 // What each variant carries: the region half of the concatenation (model.py:153,157) and the
@@ -700,21 +652,11 @@ struct Consts16 {
   static constexpr size_t BYTES = size_t(A16) * 16 + size_t(ADIST) * 4 + size_t(EPI) * 4 + 64;
 };
 
-#ifndef NAIS_RELU_MAXIMUM3
-#define NAIS_RELU_MAXIMUM3 1
-#endif
-// ReLU that keeps every NaN, as torch.relu (model.py:71). Default: gfx950's v_maximum3_f32 (IEEE
-// 754-2019 maximum: NaN propagates, max(-0, +0) = +0), one VALU. A/B (NAIS_RELU_MAXIMUM3=0): on the
-// float bits, as int32, negative
-// non-NaN floats (-0 .. -inf) are <= 0xFF800000 = -8388608 -> 0.0f; positive values (>= 0) and
-// NaNs of either sign (0xFF800001..0xFFFFFFFF = -8388607..-1) pass unchanged. v_cmp + v_cndmask;
-// a v_max_i32 alone would zero a NaN whose sign bit is set.
+// ReLU that keeps every NaN, as torch.relu (model.py:71): gfx950's v_maximum3_f32 (IEEE 754-2019
+// maximum: NaN propagates, max(-0, +0) = +0), one VALU. (The round-2 form, v_cmp + v_cndmask on
+// the float bits, was 1.1 % slower on the pair table: profiles/r3/relu_ab.)
 __device__ __forceinline__ float relu_bits(float v) {
-#if NAIS_RELU_MAXIMUM3
   return __builtin_elementwise_maximum(v, 0.f);   // v_maximum3_f32: IEEE maximum, NaN in -> NaN out
-#else
-  return (__float_as_int(v) >= -8388607) ? v : 0.f;
-#endif
 }
 
 template <int HB, bool REGS>
@@ -1012,65 +954,35 @@ catalog_score_x3_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // candidate into B fragments that stay in VGPRs for the whole sweep. The per-(c, j) VALU work
 // is then only the epilogue and h_j . t_c -- no per-pair conversions.
 // ---------------------------------------------------------------------------------------------
-#ifndef NAIS_X3B_PIPE6
-#define NAIS_X3B_PIPE6 1
-#endif
-#ifndef NAIS_X3B_WLDS
-#define NAIS_X3B_WLDS 1
-#endif
 template <int DH, int HB, bool DIST, int NW = WAVES, int NPC = 2>
 struct CfgB {
   static constexpr int D = 2 * DH;
   static constexpr int KS = DH / 8;
   static constexpr int NE = HB * KS * 64;             // uint4 fragment entries per item and piece
   static constexpr int IB = NE * 16 * NPC;            // bytes per item (all pieces)
-#ifdef NAIS_X3B_G
-  static constexpr int G = NAIS_X3B_G;
-#else
-#ifdef NAIS_X3B_G6   // A/B: items per ring group of the fp16x6 kernels
-  static constexpr int G = NPC == 3 ? NAIS_X3B_G6 : (IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1));
-#else
   static constexpr int G = IB <= 16384 ? 4 : (IB <= 32768 ? 2 : 1);   // items per ring group
-#endif
-#endif
-  // LDS chunk rows; fp16x6 keeps 32 (the s tile below) even where 64 would fit
-#ifndef NAIS_X3B_JCB6
-#define NAIS_X3B_JCB6 32   // A/B: 64-row chunks for fp16x6 (needs NAIS_X3B_SMFMA=0: the s tile is 32 rows)
-#endif
-  static constexpr int JCB = (NPC == 3) ? NAIS_X3B_JCB6 : (2 * G * IB + 64 * D * 4 > 140 * 1024 ? 32 : 64);
+  // LDS chunk rows; fp16x6 keeps 32 (the s tile below) even where 64 would fit (64-row chunks
+  // without the s tile: -1..-3 %, profiles/r2/jcb_ab)
+  static constexpr int JCB = (NPC == 3) ? 32 : (2 * G * IB + 64 * D * 4 > 140 * 1024 ? 32 : 64);
   static constexpr int EPT = (NE + NW * 64 - 1) / (NW * 64);  // build entries per thread
   static constexpr int ADIST = DIST ? HB * 64 : 0;
   static constexpr int EPI = 2 * 2 * HB * 16;
   // PIPE: the epilogue of item j-1 interleaved with item j's MFMAs (two accumulator sets, b1 / w2
   // in VGPRs) -- fits 256 VGPRs for D, H <= 64. Wider: one accumulator set, epilogue right after
   // the item's MFMAs (the SIMD's other wave overlaps it), b1 / w2 read from LDS (Epi16<HB, false>).
-#ifdef NAIS_X3B_NOPIPE
-  static constexpr bool PIPE = false;   // debug: the wide epilogue structure for every shape
-#else
   // fp16x6 (NPC = 3) pipelines too, with b1 / w2 read from LDS (EREGS = false) to stay within
   // 256 VGPRs; without the pipeline the per-group barrier lines up both waves of a SIMD, so their
   // MFMA and VALU phases coincide instead of overlapping
-  static constexpr bool PIPE = (NPC == 2 || NAIS_X3B_PIPE6) && HB <= 2 && DH <= 32;
-#endif
+  static constexpr bool PIPE = HB <= 2 && DH <= 32;
   static constexpr bool EREGS = PIPE && NPC == 2;   // b1 / w2 pre-scaled in VGPRs
   // fp16x6 pipeline: one candidate scale S_t per WAVE (not per lane), so S = S_A * S_t is
   // wave-uniform and each wave keeps S*b1 and w2/S in its own LDS slot (Epi16L): acc starts at
   // S*b1 and the epilogue is relu + fma (3 VALU per value instead of 4), no VGPRs spent
-  static constexpr bool WLDS = NAIS_X3B_WLDS && PIPE && !EREGS;
+  static constexpr bool WLDS = PIPE && !EREGS;
   static constexpr int ESCL = WLDS ? NW * EPI : 0;
   static constexpr size_t REST = size_t(ADIST) * 4 + size_t(EPI) * 4 + size_t(ESCL) * 4 + 64 +
                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + (DIST ? size_t(JCB) * 16 : 0);
-  // RING1: one ring slot instead of two (fp16x6 at D = H = 128: a 96 KiB item, 2 x 96 KiB do not
-  // fit the 160 KiB LDS) -- build item j, barrier, every wave's MFMAs on it, barrier; the builds
-  // then do not overlap the matrix work, but the A_j build stays once per item and workgroup
-  // (the per-pair split kernel splits x = h (.) t for every pair instead)
-#ifndef NAIS_X3B_RING1
-#define NAIS_X3B_RING1 0   // A/B (round 3): 8.79 vs 8.67 ms per D = H = 128 table block, config-5 direct 6.71e7 vs 6.60e7 pairs/s -- a wash
-#endif
-  static constexpr size_t LDS_MAX = 160 * 1024;
-  static constexpr bool RING1 = NAIS_X3B_RING1 && !PIPE && G == 1 &&
-                                size_t(2) * IB + REST > LDS_MAX && size_t(IB) + REST <= LDS_MAX;
-  static constexpr size_t BYTES = size_t(RING1 ? 1 : 2) * G * IB + REST;
+  static constexpr size_t BYTES = size_t(2) * G * IB + REST;
   static_assert(!PIPE || G % 2 == 0, "the pipelined steps alternate two accumulator sets per item");
 };
 
@@ -1090,13 +1002,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   constexpr bool PIPE = C::PIPE;
   // s = h_j . t_c for the chunk's 32 items on the matrix pipe (one 32x32 tile per wave and chunk,
   // the same split-fp16 3-product scheme) instead of a 2*DH-term VALU dot per item and lane
-#ifndef NAIS_X3B_SMFMA
-#define NAIS_X3B_SMFMA 1
-#endif
-  constexpr bool SMF = NAIS_X3B_SMFMA && JCB == 32;
+  constexpr bool SMF = JCB == 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups (1: RING1)][G items][piece][NE]
-  float* Adist = reinterpret_cast<float*>(ring + (C::RING1 ? 1 : 2) * G * NPC * NE);
+  uint4* ring = reinterpret_cast<uint4*>(smem);       // [2 groups][G items][piece][NE]
+  float* Adist = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);
   float* Eimg = Adist + C::ADIST;
   float* Escl = Eimg + C::EPI;          // WLDS: per wave [S*b1 | w2/S] (EPI floats each)
   float* red = Escl + C::ESCL;
@@ -1312,7 +1221,6 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
           sd = __builtin_fmaf(tv[4 * q + 3], hv.w, sd);
         }
       }
-      if (NAIS_X3B_SCHED) __builtin_amdgcn_sched_barrier(0);
     }
     if (DIST && MMA) {   // the 2 distance columns of item `cur`: exact fp32 MFMA K-step
       float ll0, ll1;
@@ -1439,15 +1347,6 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     } else {
       epi.rescale(Eimg, hh, Sacc, invS);
     }
-    if constexpr (C::RING1) {   // one slot: build, barrier, consume, barrier
-      for (int jj = 0; jj < jn; ++jj) {
-        if (jj > 0) __syncthreads();   // every wave is done with item jj - 1 (the slot's tenant)
-        build(jj, 0, 0);
-        __syncthreads();
-        step_wide(ring, jj);
-      }
-      continue;   // the next chunk's (or the exit's) barrier orders the last item's reads
-    }
     const int ngroups = (jn + G - 1) / G;
 #pragma unroll
     for (int it = 0; it < G; ++it)
@@ -1455,7 +1354,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
     __syncthreads();
     int prev = -1;                      // chunk-local item whose epilogue is pending in accP
     for (int g = 0; g < ngroups; ++g) {
-      if ((PIPE || !NAIS_X3B_WIDE_ILV) && g + 1 < ngroups) {
+      if (g + 1 < ngroups) {
 #pragma unroll
         for (int it = 0; it < G; ++it) {
           const int jj = (g + 1) * G + it;
@@ -1472,15 +1371,11 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
                  prev >= 0);
             prev = jj;
           } else {
-            if (NAIS_X3B_WIDE_ILV && g + 1 < ngroups && (g + 1) * G + it < jn)
-              build((g + 1) * G + it, (g + 1) & 1, it);   // next group's A_j beside this MFMA chain
             step_wide(src, jj);
           }
         }
       }
-#ifndef NAIS_X3B_DIAG_NOGROUPBAR   // timing-only diagnostic build: the ring then races
       __syncthreads();
-#endif
     }
     if (PIPE && prev >= 0) {   // drain: epilogue of the chunk's last item, no MFMAs
       if (prev & 1)
@@ -1500,317 +1395,6 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
   if (nan_count) {
     const unsigned long long m = __ballot(valid && hh == 0 && !in_hist && isnan_);
     if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Pair-table kernel "x3c": fp16x6, D = H = 64, NAIS_basic (model.py:57-89 per pair; the headline
-// job's table). The x3b item-side factorisation A_j t_c with ONE wave per SIMD and 64 candidates
-// per wave (two 32-column tiles that share the A_j ring):
-//  * 4 waves x 64 candidates = the same 256 candidates per workgroup, so the A_j build is shared
-//    as in x3b, but each SIMD runs a single instruction stream: the tile-0 MFMA chain of item j
-//    carries the epilogue of tile 1 of item j-1, the tile-1 chain carries tile 0's epilogue of
-//    item j (one accumulator set per tile);
-//  * S*b1 (each chain's first src C) and w2/S live in VGPRs: the epilogue reads no LDS and is two
-//    VALU per value (v_maximum3_f32, a ReLU that keeps NaN as torch.relu does, + fma);
-//  * the next group's A_j is built in slices between the MFMAs instead of as a burst before them;
-//  * the pair's two table entries leave as one store per tile (lane half 0: e, half 1: e*s).
-// Same pieces, products and per-hidden-block accumulation order as x3b; the candidate scale is
-// per wave (64 candidates) instead of per 32, which changes results only where a piece falls into
-// fp16 subnormals (below 2^-37 of the scaled maximum).
-// ---------------------------------------------------------------------------------------------
-// A/B (round 3, profiles/r3/x3c_ab): bit-identical tables to x3b on the config-4 block, 186 pair /
-// fp16x6 / config parity tests green, but 2.41 vs 2.20 ms per 512-column block at J = 100k (-9 %):
-// at one wave per SIMD every LDS-read and barrier wait idles the matrix core, which x3b's second
-// wave per SIMD covers; the lighter instruction stream (2 VALU per epilogue value, half the A_j
-// reads per pair, no epilogue-constant LDS reads in the unpinned form) does not make up for it.
-#ifndef NAIS_X3C
-#define NAIS_X3C 0   // 1 = the fp16x6 D = H = 64 NAIS_basic pair table on x3c instead of x3b
-#endif
-namespace x3c {
-constexpr int NW = 4, TPW = 2, CPB = NW * TPW * 32;   // waves, tiles per wave, candidates per WG
-constexpr int DH = 32, D = 64, HB = 2, KS = 4, NPC = 3;
-constexpr int NE = HB * KS * 64;                       // uint4 fragment entries per item and piece
-constexpr int G = 2, JCB = 32;                         // items per ring group, chunk rows
-constexpr int EPT = NE / (NW * 64);                    // build entries per thread and item (2)
-constexpr int NU = HB * KS;                            // (s, hb) units per tile chain
-constexpr int EPI = 2 * 2 * HB * 16;                   // [b1 | w2][lane half][HB * 16]
-constexpr int SV = NW * TPW * 16 * 64;                 // s tiles in LDS: [wave][tile][reg][lane]
-constexpr size_t BYTES = size_t(2) * G * NPC * NE * 16 + size_t(JCB) * D * 4 + size_t(EPI) * 4 +
-                         64 + size_t(JCB) * 4 + size_t(SV) * 4 + size_t(NW) * EPI * 4;
-static_assert(EPT == TPW, "one build entry per tile phase");
-}  // namespace x3c
-
-__device__ __forceinline__ float relu_keepnan(float v) {
-  return __builtin_elementwise_maximum(v, 0.f);   // v_maximum3_f32: NaN in, NaN out; -0 -> +0
-}
-
-__global__ void __launch_bounds__(x3c::NW * 64, 1)
-pair_table_x3c_kernel(DevParams p, const int64_t* __restrict__ indices, TableOut tab) {
-  using namespace x3c;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);                        // [2][G][NPC][NE]
-  float* hrows = reinterpret_cast<float*>(ring + 2 * G * NPC * NE);   // [JCB][D]
-  float* Eimg = hrows + JCB * D;
-  float* red = Eimg + EPI;
-  int32_t* hid = reinterpret_cast<int32_t*>(red + 16);
-  float* svt = reinterpret_cast<float*>(hid + JCB);                   // [NW][TPW][16][64]
-  float* escl = svt + SV;   // per wave: [S*b1 | w2/S][lane half][HB * 16] (S is wave-uniform)
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5;
-  const int64_t hbeg = (int64_t)blockIdx.y * tab.gi;
-  const int64_t hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
-  int64_t cand[TPW];
-  bool valid[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    cand[t] = tab.col0 + (int64_t)blockIdx.x * CPB + wave * 64 + t * 32 + (lane & 31);
-    valid[t] = cand[t] < p.P && cand[t] < tab.col0 + tab.cols;
-  }
-
-  // ---- this thread's W1 values for its build entries (fp32; pre-scaled by S_A per chunk)
-  float wv[EPT][8];
-  float wmax = 0.f;
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * NW * 64;
-    const int ln = e & 63, s = (e >> 6) % KS, hb = (e >> 6) / KS;
-    const int i = hb * 32 + (ln & 31), k0 = (ln >> 5) * DH + 8 * s;
-#pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      wv[q][x] = p.w1[(int64_t)i * p.din + k0 + x];
-      wmax = fmaxf(wmax, fabsf(wv[q][x]));
-    }
-  }
-  for (int f = tid; f < EPI; f += NW * 64) {
-    const int which = f / (2 * HB * 16), rem = f % (2 * HB * 16);
-    const int hh2 = rem / (HB * 16), hr = rem % (HB * 16);
-    const int i = acc_row(hr / 16, hr % 16, hh2);
-    Eimg[f] = which == 0 ? p.b1[i] : p.w2[i];
-  }
-  const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg
-
-  // ---- candidate operands: both tiles scaled by one S_t per wave, split into B fragments
-  half8 tb[TPW][KS][NPC];
-  float St;
-  {
-    float tv[TPW][DH];
-    float tmax = 0.f;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const float* src = p.et + (valid[t] ? cand[t] : p.P - 1) * p.item_dim + hh * DH;
-#pragma unroll
-      for (int q = 0; q < DH / 4; ++q) {
-        const float4 v = reinterpret_cast<const float4*>(src)[q];
-        tv[t][4 * q] = v.x;
-        tv[t][4 * q + 1] = v.y;
-        tv[t][4 * q + 2] = v.z;
-        tv[t][4 * q + 3] = v.w;
-      }
-#pragma unroll
-      for (int k = 0; k < DH; ++k) tmax = fmaxf(tmax, fabsf(tv[t][k]));
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
-    St = pow2_scale(tmax);
-#pragma unroll
-    for (int t = 0; t < TPW; ++t)
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = tv[t][8 * s + e] * St;
-        split_pieces<NPC>(x, tb[t][s]);
-      }
-  }
-
-  floatx16 acc[TPW][HB];
-  const float* bS = escl + wave * EPI + hh * HB * 16;                // S*b1 of this lane's rows
-  const float* wS = escl + wave * EPI + 2 * HB * 16 + hh * HB * 16;  // w2/S of the same rows
-  float SAcur = 1.f;
-  int64_t j0 = 0;
-
-  // build entry q of chunk-local item jj into ring slot dst (all pieces)
-  auto build = [&](int jj, uint4* dst, int q) {
-    const int e = tid + q * NW * 64;
-    const int ln = e & 63, s = (e >> 6) % KS;
-    const float* hr = hrows + jj * D + (ln >> 5) * DH + 8 * s;
-    const float4 h0 = *reinterpret_cast<const float4*>(hr);
-    const float4 h1 = *reinterpret_cast<const float4*>(hr + 4);
-    float a[8];
-    a[0] = wv[q][0] * h0.x;
-    a[1] = wv[q][1] * h0.y;
-    a[2] = wv[q][2] * h0.z;
-    a[3] = wv[q][3] * h0.w;
-    a[4] = wv[q][4] * h1.x;
-    a[5] = wv[q][5] * h1.y;
-    a[6] = wv[q][6] * h1.z;
-    a[7] = wv[q][7] * h1.w;
-    half8 pc[NPC];
-    split_pieces<NPC>(a, pc);
-#pragma unroll
-    for (int q2 = 0; q2 < NPC; ++q2) dst[q2 * NE + e] = *reinterpret_cast<const uint4*>(&pc[q2]);
-  };
-
-  // the pair (chunk item pj, tile t): e and e*s from the attention-logit partial ap
-  auto tail = [&](int t, int pj, float ap) {
-    const float2 aph = lane_halves(ap);
-    const float a = aph.x + aph.y;
-    // item pj's row of the s tile: register ((pj/8)*4 + pj%4) of lane half (pj/4)%2
-    const float sv = svt[((wave * TPW + t) * 16 + (((pj >> 3) << 2) | (pj & 3))) * 64 +
-                         ((pj >> 2) & 1) * 32 + (lane & 31)];
-    const bool keep = hid[pj] != (int32_t)cand[t];
-    const float e = expf(a) * (keep ? 1.f : 0.f);
-    if (valid[t]) {
-      const int64_t o = (hbeg + j0 + pj) * tab.ld + (cand[t] - tab.col0);
-      if (hh == 0) tab_store(tab.e + o, e);
-      else tab_store(tab.es + o, e * sv);
-    }
-  };
-
-  // One phase: tile T's MFMA chain for the item in ring slot src (MMA), the epilogue + tail of
-  // tile 1 - T for chunk item ej (ej >= 0), and (MMA) build entry T of chunk item bj into slot
-  // bdst, in NU units of (6 MFMAs + 4 epilogue values + a build slice)
-  auto phase = [&](auto Tc, auto MMAc, const uint4* src, int ej, int bj, uint4* bdst) {
-    constexpr int T = decltype(Tc)::value, O = 1 - T;
-    constexpr bool MMA = decltype(MMAc)::value;
-    float ap = 0.f;
-    uint4 an[NPC];
-    if constexpr (MMA) {
-#pragma unroll
-      for (int q = 0; q < NPC; ++q) an[q] = src[q * NE + lane];
-    }
-    float4 h0, h1;
-    float a8[8];
-    const int be = tid + T * NW * 64;
-    const int bln = be & 63, bs = (be >> 6) % KS;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int s = u / HB, hb = u % HB;
-      if constexpr (MMA) {
-        half8 a_[NPC];
-#pragma unroll
-        for (int q = 0; q < NPC; ++q) a_[q] = *reinterpret_cast<const half8*>(&an[q]);
-        if (u + 1 < NU) {
-          const int s2 = (u + 1) / HB, hb2 = (u + 1) % HB;
-#pragma unroll
-          for (int q = 0; q < NPC; ++q) an[q] = src[q * NE + (hb2 * KS + s2) * 64 + lane];
-        }
-        if (s == 0) {   // the chain starts at S*b1 (4 broadcast ds_read_b128 per lane half)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[T][hb][r] = bS[hb * 16 + r];
-        }
-        acc[T][hb] = mfma_pieces<NPC>(a_, tb[T][s], acc[T][hb]);
-      }
-#pragma unroll
-      for (int v = u * 4; v < u * 4 + 4; ++v)
-        ap = __builtin_fmaf(wS[v], relu_keepnan(acc[O][v / 16][v % 16]), ap);
-      asm volatile("" : "+v"(ap));   // keep the slice in this unit (else it sinks to the tail)
-      if constexpr (MMA) {   // every item step builds; a slot built for a row past jn is never read
-        if (u == 1) {
-          const float* hr = hrows + bj * D + (bln >> 5) * DH + 8 * bs;
-          h0 = *reinterpret_cast<const float4*>(hr);
-          h1 = *reinterpret_cast<const float4*>(hr + 4);
-        } else if (u == 2) {
-          a8[0] = wv[T][0] * h0.x;
-          a8[1] = wv[T][1] * h0.y;
-          a8[2] = wv[T][2] * h0.z;
-          a8[3] = wv[T][3] * h0.w;
-          a8[4] = wv[T][4] * h1.x;
-          a8[5] = wv[T][5] * h1.y;
-          a8[6] = wv[T][6] * h1.z;
-          a8[7] = wv[T][7] * h1.w;
-        } else if (u == 4) {
-          half8 pc[NPC];
-          split_pieces<NPC>(a8, pc);
-#pragma unroll
-          for (int q2 = 0; q2 < NPC; ++q2) bdst[q2 * NE + be] = *reinterpret_cast<const uint4*>(&pc[q2]);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (ej >= 0) tail(O, ej, ap);
-  };
-
-  for (j0 = 0; j0 < hlen; j0 += JCB) {
-    const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
-    __syncthreads();   // the previous chunk's ring, hrows and hid readers are done
-    float hmax = 0.f;
-    for (int f = tid; f < jn * (D / 4); f += NW * 64) {
-      const int jj = f / (D / 4), q4 = f % (D / 4);
-      const int64_t item = indices[hbeg + j0 + jj];
-      const float4 v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
-      reinterpret_cast<float4*>(hrows)[f] = v;
-      hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
-    for (int jj = tid; jj < jn; jj += NW * 64) hid[jj] = (int32_t)indices[hbeg + j0 + jj];
-    const float Hm = block_max_n<NW>(hmax, red);   // barrier: chunk published
-    const float SA = pow2_scale(Wmax * Hm);
-    const float rs = SA / SAcur;                   // exact power-of-two ratio
-#pragma unroll
-    for (int q = 0; q < EPT; ++q)
-#pragma unroll
-      for (int x = 0; x < 8; ++x) wv[q][x] *= rs;
-    SAcur = SA;
-    const float Sacc = SA * St, invS = 1.f / Sacc;
-    for (int f = lane; f < EPI; f += 64)   // this wave's S*b1 and w2/S (published by the barrier below)
-      escl[wave * EPI + f] = Eimg[f] * (f < 2 * HB * 16 ? Sacc : invS);
-    {   // s tiles: rows = the chunk's items (pieces of h * S_h), columns = the tiles' candidates;
-        // kept in LDS (this wave's own region) as s = tile value / (S_h S_t)
-      const float Sh = pow2_scale(Hm);
-      const float invShSt = 1.f / (Sh * St);
-      const int m = lane & 31;
-      floatx16 sacc[TPW];
-#pragma unroll
-      for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[t][r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        float x[8];
-        const float* hp = hrows + m * D + hh * DH + 8 * s;
-        const float4 h0 = *reinterpret_cast<const float4*>(hp);
-        const float4 h1 = *reinterpret_cast<const float4*>(hp + 4);
-        const bool ok = m < jn;
-        x[0] = ok ? h0.x * Sh : 0.f; x[1] = ok ? h0.y * Sh : 0.f;
-        x[2] = ok ? h0.z * Sh : 0.f; x[3] = ok ? h0.w * Sh : 0.f;
-        x[4] = ok ? h1.x * Sh : 0.f; x[5] = ok ? h1.y * Sh : 0.f;
-        x[6] = ok ? h1.z * Sh : 0.f; x[7] = ok ? h1.w * Sh : 0.f;
-        half8 hpc[NPC];
-        split_pieces<NPC>(x, hpc);
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) sacc[t] = mfma_pieces<NPC>(hpc, tb[t][s], sacc[t]);
-      }
-#pragma unroll
-      for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) svt[((wave * TPW + t) * 16 + r) * 64 + lane] = sacc[t][r] * invShSt;
-    }
-    const int ngroups = (jn + G - 1) / G;
-#pragma unroll
-    for (int it = 0; it < G; ++it)
-      if (it < jn)
-#pragma unroll
-        for (int q = 0; q < EPT; ++q) build(it, ring + (it * NPC) * NE, q);
-    __syncthreads();
-    int prev = -1;   // chunk-local item whose tile-1 epilogue is pending in acc[1]
-    for (int g = 0; g < ngroups; ++g) {
-#pragma unroll
-      for (int it = 0; it < G; ++it) {
-        const int jj = g * G + it;
-        if (jj < jn) {
-          const uint4* src = ring + (((g & 1) * G + it) * NPC) * NE;
-          const int bj = ((g + 1) * G + it) & (JCB - 1);   // rows past jn: stale, never read
-          uint4* bdst = ring + ((((g + 1) & 1) * G + it) * NPC) * NE;
-          phase(std::integral_constant<int, 0>{}, std::true_type{}, src, prev, bj, bdst);
-          phase(std::integral_constant<int, 1>{}, std::true_type{}, src, jj, bj, bdst);
-          prev = jj;
-        }
-      }
-      __syncthreads();
-    }
-    if (prev >= 0)   // drain: tile 1's epilogue of the chunk's last item, no MFMAs
-      phase(std::integral_constant<int, 0>{}, std::false_type{}, ring, prev, 0, ring);
   }
 }
 
@@ -2330,17 +1914,13 @@ distance_histogram_kernel(const double* __restrict__ coords, const int64_t* __re
 // ---------------------------------------------------------------------------------------------
 // Standalone row gather (HBM roofline kernel): 16 B per lane, one row per dim/4 lanes.
 // ---------------------------------------------------------------------------------------------
-#ifndef NAIS_GATHER_UNROLL
-#define NAIS_GATHER_UNROLL 1
-#endif
-// Each thread moves NAIS_GATHER_UNROLL float4 pieces (from U different rows) per iteration: all
-// loads are issued before the stores, so every lane keeps U x 16 B in flight; rows are read once
-// and written once, so both sides use non-temporal (streaming) accesses.
+// Each thread moves one float4 piece per iteration; rows are read once and written once, so both
+// sides use non-temporal (streaming) accesses.
 typedef float nf4 __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(256)
 gather_rows_kernel(const nf4* __restrict__ table, int q4, const int64_t* __restrict__ idx,
                    int64_t m, nf4* __restrict__ out) {
-  constexpr int U = NAIS_GATHER_UNROLL;
+  constexpr int U = 1;
   const int64_t total = m * q4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2515,8 +2095,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
-  } else if constexpr ((VarT<VAR>::DIST && !(NAIS_X3B_DIST && CfgB<DH, HB, true, NAIS_X3B_NW, NPC>::PIPE)) ||
-                       (NAIS_X3B_WIDE == 0 && !(HB <= 2 && DH <= 32)) ||
+  } else if constexpr ((VarT<VAR>::DIST && !CfgB<DH, HB, true, WAVES, NPC>::PIPE) ||
                        CfgB<DH, HB, false, WAVES, NPC>::BYTES > kLdsBytes) {
     // the distance features ride on the per-pair split kernel (also in pair-table mode) except on
     // the pipelined item-side shapes (D, H <= 64), whose step adds them as one exact fp32 MFMA
@@ -2524,7 +2103,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     return launch_catalog_x3<DH, HB, VAR, NPC>(d, indptr, indices, users, nb, region_of, coords,
                                                latlon_mat, scores, ld, nan_count, stream, tab);
   } else {
-    constexpr int NW = NAIS_X3B_NW;   // A/B: 4 = two 4-wave workgroups per CU (barriers decoupled)
+    constexpr int NW = WAVES;
     const size_t lds = CfgB<DH, HB, VarT<VAR>::DIST, NW, NPC>::BYTES;
     auto kern = catalog_score_x3b_kernel<DH, HB, VAR, NW, NPC>;
     static bool attr_set = false;
@@ -2607,13 +2186,9 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Every pr_d(d) = a * max(0.01, d)^b is finite and >= +0 for d in powerLaw.dist's range
 // [0, pi * 6371] (a NaN distance takes the 0.01 branch): a > 0 and both ends finite (pr_d is
 // monotone in d). Then a G product at +0.0 stays +0.0. The host-side twin for the pairs route is
-// catalog._prior_entries_finite. NAIS_PRIOR_EXIT=0 turns the exit off (A/B).
+// catalog._prior_entries_finite.
 bool prior_zero_exit(double a, double b) {
-  static const bool on = [] {
-    const char* e = std::getenv("NAIS_PRIOR_EXIT");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || !std::isfinite(a) || !std::isfinite(b) || !(a > 0.0)) return false;
+  if (!std::isfinite(a) || !std::isfinite(b) || !(a > 0.0)) return false;
   const double lo = a * std::pow(0.01, b), hi = a * std::pow(3.141592653589793 * 6371.0, b);
   return std::isfinite(lo) && std::isfinite(hi);
 }
@@ -2753,21 +2328,18 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
 }
 
 namespace {
-// nais_pair_table / nais_pair_table_il: cs = 0 -> two row-major tables (e, es, ld), cs > 0 -> one
-// interleaved chunk-major table (e; es unused)
+// nais_pair_table: two row-major tables (e, es) with row pitch ld
 int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64_t num_items,
                         int64_t col0, int64_t cols, const int64_t* region_of, const double* coords,
-                        const double* latlon_mat, float* e, float* es, int64_t ld, int64_t cs,
-                        void* stream) {
+                        const double* latlon_mat, float* e, float* es, int64_t ld, void* stream) {
   Shape sh;
   int rc = validate(params, &sh);
   if (rc) return rc;
   if (num_items < 0 || col0 < 0 || cols < 0 || col0 + cols > params->num_pois)
     return fail(NAIS_E_INVALID, "bad item count or column range");
   if (num_items == 0 || cols == 0) return NAIS_OK;
-  if (!items || !e || (!cs && !es)) return fail(NAIS_E_INVALID, "missing pointer");
-  if (!cs && ld < cols) return fail(NAIS_E_INVALID, "ld < cols");
-  if (cs && cs < num_items * 128) return fail(NAIS_E_INVALID, "chunk_stride < num_items * 128");
+  if (!items || !e || !es) return fail(NAIS_E_INVALID, "missing pointer");
+  if (ld < cols) return fail(NAIS_E_INVALID, "ld < cols");
   if ((params->variant == NAIS_VARIANT_REGION || params->variant == NAIS_VARIANT_REGION_DISTANCE) &&
       !region_of)
     return fail(NAIS_E_INVALID, "region variants need region_of");
@@ -2781,29 +2353,16 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
   TableOut tab;
   tab.ld = ld;
   tab.cols = cols;
-  tab.cs = cs;
   tab.gi = PAIR_GROUP_ITEMS;
   const int64_t groups_per_launch = 65535;
   for (int64_t g0 = 0; g0 * tab.gi < num_items; g0 += groups_per_launch) {
     const int64_t base = g0 * tab.gi;
     tab.nitems = std::min<int64_t>(num_items - base, groups_per_launch * tab.gi);
-    tab.e = e + base * (cs ? 128 : ld);
-    tab.es = cs ? nullptr : es + base * ld;
+    tab.e = e + base * ld;
+    tab.es = es + base * ld;
     tab.col0 = col0;
     const int ng = (int)((tab.nitems + tab.gi - 1) / tab.gi);
-    if (NAIS_X3C && params->precision == NAIS_PRECISION_FP16X6 &&
-        params->variant == NAIS_VARIANT_BASIC && params->embed_dim == 64 && params->hidden == 64 &&
-        cs == 0) {
-      static bool attr_set = false;
-      if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pair_table_x3c_kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3c::BYTES);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL(pair_table_x3c_kernel, table_grid(tab, ng, x3c::CPB), dim3(x3c::NW * 64),
-                         x3c::BYTES, st, d, items + base, tab);
-      rc = check_launch("pair_table_x3c_kernel");
-    } else if (params->precision == NAIS_PRECISION_FP32)
+    if (params->precision == NAIS_PRECISION_FP32)
       NAIS_DISPATCH(launch_catalog, sh.DH, sh.HB, params->variant, d, nullptr, items + base, nullptr,
                     ng, region_of, coords, latlon_mat, nullptr, 0, nullptr, st, tab);
     else if (params->precision == NAIS_PRECISION_FP16X6 ||
@@ -2824,16 +2383,7 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
                         const double* coords, const double* latlon_mat, float* e, float* es,
                         int64_t ld, void* stream) {
   return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, e, es,
-                         ld, 0, stream);
-}
-
-int32_t nais_pair_table_il(const nais_params_t* params, const int64_t* items, int64_t num_items,
-                           int64_t col0, int64_t cols, const int64_t* region_of,
-                           const double* coords, const double* latlon_mat, float* table,
-                           int64_t chunk_stride, void* stream) {
-  if (chunk_stride <= 0) return fail(NAIS_E_INVALID, "chunk_stride must be > 0");
-  return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, table,
-                         nullptr, 0, chunk_stride, stream);
+                         ld, stream);
 }
 
 int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,

@@ -27,23 +27,14 @@
 
 namespace {
 
-#ifndef NAIS_GATHER_NT_STORE
-#define NAIS_GATHER_NT_STORE 0   // 1: non-temporal score stores (A/B: keep the stripe in the Infinity Cache)
-#endif
-#ifndef NAIS_GATHER_CPL
-#define NAIS_GATHER_CPL 4   // columns per lane: stripe = 64 * CPL columns (A/B knob)
-#endif
-constexpr int CPL = NAIS_GATHER_CPL;
+// Columns per lane: stripe = 64 * CPL columns. (A/B, profiles/r1/: 2 columns per lane -- a
+// 128-column stripe -- 654 vs 560 ms per job, 8 per lane -- 512 columns, 410 MB of stripe, past
+// the Infinity Cache -- 845 ms; non-temporal table loads -15 %, non-temporal score stores +-1 %.)
+constexpr int CPL = 4;
 typedef float nfv __attribute__((ext_vector_type(CPL)));
 typedef double ndv __attribute__((ext_vector_type(CPL)));
 
-#ifndef NAIS_GATHER_NT
-#define NAIS_GATHER_NT 0   // 1: non-temporal table loads (slower: the Infinity Cache then holds nothing)
-#endif
-__device__ __forceinline__ nfv loadv(const float* p) {
-  if (NAIS_GATHER_NT) return __builtin_nontemporal_load(reinterpret_cast<const nfv*>(p));
-  return *reinterpret_cast<const nfv*>(p);
-}
+__device__ __forceinline__ nfv loadv(const float* p) { return *reinterpret_cast<const nfv*>(p); }
 
 constexpr int SCAN_THREADS = 1024;
 
@@ -126,10 +117,7 @@ place_kernel(int32_t* __restrict__ flag_rowmap, int64_t P, const int32_t* __rest
 // stripe of the tables -- J x 256 x 8 B, ~200 MB at J = 100k -- so the Infinity Cache serves the
 // rows the ~50 users sharing each item read (A/B: profiles/r1/pairs/). N and S are summed in
 // history (CSR) order, then the score of model.py:55 / validation.py:26; history POIs get -1.
-#ifndef NAIS_GATHER_GW
-#define NAIS_GATHER_GW 4
-#endif
-constexpr int GW = NAIS_GATHER_GW;          // users (waves) per workgroup
+constexpr int GW = 4;                       // users (waves) per workgroup (1 / 2 / 8: +-1 %)
 
 // lane jj's 64-bit value, as a wave-uniform scalar (readlane returns int: widen via uint32_t)
 __device__ __forceinline__ int64_t bcast64(uint32_t lo, uint32_t hi, int jj) {
@@ -143,10 +131,7 @@ constexpr int STRIPE = 64 * CPL;             // columns per wave
 // count does not unroll here (the loop holds convergent readlanes), which left one row -- 2 KB per
 // wave -- in flight and the gather latency-bound; GU explicit loads per step keep GU rows in flight
 // while the adds stay in history (CSR) order.
-#ifndef NAIS_GATHER_UNROLL
-#define NAIS_GATHER_UNROLL 8
-#endif
-constexpr int GU = NAIS_GATHER_UNROLL;
+constexpr int GU = 8;
 
 // Sa += Σ E[row(j), x..x+CPL), Na += Σ ES[...] over the jn (wave-uniform) rows whose offsets the
 // lanes 0..jn-1 hold in (mlo, mhi), in lane order. Full CPL-column vectors only.
@@ -227,8 +212,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
         sc = __builtin_nanf("");
         ++nan;
       }
-      if (NAIS_GATHER_NT_STORE) __builtin_nontemporal_store(sc, out + q);
-      else out[q] = sc;
+      out[q] = sc;
     }
   }
   __threadfence_block();   // this wave's score stores land before its -1 stores below
@@ -383,197 +367,6 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
   const int nk = n < k ? n : k;
   for (int i = lane; i < nk; i += 64) keys[slot * k + i] = L[i];
   if (lane == 0) kcount[slot] = nk;
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// L2-blocked fused gather + running top-k (an A/B knob, off by default: 2-3x slower):
-// one launch per 64-column chunk of an interleaved chunk-major table (nais_pair_table_il: the
-// pair (row r, column x) at table[(x / 64) * cs + r * 128 + (x % 64) * 2] = (e, es), 512 B per
-// row and chunk). A wave owns up to UPW users (slots gw, gw + nwaves, ...: an even mix of the
-// longest-first order) and keeps their 64 columns' sums in registers (lane = column) while it walks
-// the table in blocks of `rb_rows` rows: every user's history entries inside the block, then the
-// next block. All waves start together and do about the same work per block, so the rows in use
-// at a time are one block of ~1.5 MB per XCD -- served by the XCD's L2 instead of the Infinity
-// Cache (the one-launch-per-stripe kernel above re-reads every shared row from the fabric).
-// Requires CSR rows sorted by POI (the reference's tocsr() output, datasets.py:262): rowmap is
-// ascending in POI, so each user's rows ascend and the block walk visits its entries in CSR order
-// -- the same sums, in the same order, as pair_gather_topk_kernel and the per-user kernels.
-constexpr int L2_WAVES = 4;                   // waves per workgroup
-#ifndef NAIS_L2_UPW
-#define NAIS_L2_UPW 16
-#endif
-constexpr int L2_UPW = NAIS_L2_UPW;           // users per wave (registers: 2 + 1 VGPRs per user)
-constexpr int L2_TK = 512;                    // LDS keys per wave: pow2 >= k + 64 (k <= 256)
-
-__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
-  return bcast64(uint32_t(v), uint32_t(uint64_t(v) >> 32), l);
-}
-
-template <int UPW>
-__global__ void __launch_bounds__(L2_WAVES * 64)
-pair_gather_topk_l2_kernel(const float* __restrict__ T, int64_t nrows, int32_t rb_rows,
-                           const int32_t* __restrict__ rowmap, const int64_t* __restrict__ indptr,
-                           const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
-                           int32_t nusers, int32_t upw, int32_t nwaves, int64_t col0, int32_t cols,
-                           float beta, int k, unsigned long long* __restrict__ keys,
-                           int32_t* __restrict__ kcount, int32_t* __restrict__ nan_count) {
-  __shared__ unsigned long long lk[L2_WAVES][L2_TK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int gw = blockIdx.x * L2_WAVES + w;
-  if (gw >= nwaves) return;                  // wave-uniform; no workgroup barriers below
-  // lane i < upw: user i's slot, history base and length, entries consumed so far
-  int64_t my_hb = 0;
-  int32_t my_hl = 0, my_pos = 0;
-  if (lane < upw) {
-    const int64_t slot = gw + int64_t(lane) * nwaves;
-    if (slot < nusers) {
-      const int64_t u = users[slot];
-      my_hb = indptr[u];
-      my_hl = int32_t(indptr[u + 1] - my_hb);
-    }
-  }
-  // rows of this chunk's POIs: rm (lane = column), [R0, R1) = their row interval
-  const int32_t rm = lane < cols ? rowmap[col0 + lane] : -1;
-  int32_t lo = rm >= 0 ? rm : 0x7fffffff, hi = rm;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, __shfl_xor(lo, o));
-    hi = max(hi, __shfl_xor(hi, o));
-  }
-  const int32_t R0 = lo, R1 = hi + 1;        // empty when no column of the chunk has a row
-  const float* Tl = T + lane * 2;
-
-  float2 acc[UPW];
-  int32_t rv[UPW];   // user i's window of 64 rows (entries 64 * floor(pos / 64) ...), INT_MAX past the end
-  uint32_t hmask = 0;   // bit i: this lane's column is in user i's history
-#pragma unroll
-  for (int i = 0; i < UPW; ++i) {
-    acc[i] = make_float2(0.f, 0.f);
-    rv[i] = 0x7fffffff;
-    if (i < upw) {
-      const int32_t hl = __builtin_amdgcn_readlane(my_hl, i);
-      const int64_t hb = readlane64(my_hb, i);
-      if (lane < hl) rv[i] = rowmap[indices[hb + lane]];
-    }
-  }
-  // Per block: user i has n_i entries below the block's end in its current window; they are read
-  // in slots t = 0, 1, ...: slot t issues the t-th entry's load of every user that has one, then
-  // adds them, so a wave keeps up to UPW table rows in flight (the per-user order is unchanged).
-  for (int64_t r0 = 0; r0 < nrows; r0 += rb_rows) {
-    const int64_t rend = std::min<int64_t>(r0 + rb_rows, nrows);
-    const int32_t row_end = rend >= nrows ? 0x7fffffff : int32_t(rend);
-    bool again = true;
-    while (again) {   // more than once only when a user's 64-entry window runs out inside the block
-      again = false;
-      int32_t n[UPW], p0[UPW];
-      int32_t maxn = 0;
-#pragma unroll
-      for (int i = 0; i < UPW; ++i) {
-        const int32_t hl = __builtin_amdgcn_readlane(my_hl, i);   // 0 for i >= upw
-        const int32_t pos = __builtin_amdgcn_readlane(my_pos, i);
-        p0[i] = pos & 63;
-        // the ballot runs on every path, so every window load has landed before the slots below
-        const int32_t cnt = __popcll(__ballot(rv[i] < row_end));
-        n[i] = pos < hl ? cnt - p0[i] : 0;
-        maxn = max(maxn, n[i]);
-      }
-      for (int t = 0; t < maxn; ++t) {
-        float2 v[UPW];
-        int32_t q[UPW];
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-          if (t < n[i]) {
-            q[i] = __builtin_amdgcn_readlane(rv[i], p0[i] + t);
-            v[i] = *reinterpret_cast<const float2*>(Tl + int64_t(q[i]) * 128);
-          }
-        }
-        // the adds run on every path (a user without a t-th entry adds +0: S >= 0, and N = -0
-        // vs +0 gives the same sigmoid), so no load can still be in flight when its register is
-        // reused in the next slot
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-          const bool on = t < n[i];
-          acc[i].x += on ? v[i].x : 0.f;
-          acc[i].y += on ? v[i].y : 0.f;
-          if (on && q[i] >= R0 && q[i] < R1 && rm == q[i]) hmask |= 1u << i;   // a history POI of the chunk
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < UPW; ++i) {
-        if (n[i] > 0) {
-          const int32_t hl = __builtin_amdgcn_readlane(my_hl, i);
-          const int32_t pos = __builtin_amdgcn_readlane(my_pos, i) + n[i];
-          my_pos = lane == i ? pos : my_pos;
-          if ((pos & 63) == 0 && pos < hl) {   // the window is used up: load the next 64 entries
-            const int64_t hb = readlane64(my_hb, i);
-            rv[i] = pos + lane < hl ? rowmap[indices[hb + pos + lane]] : 0x7fffffff;
-            again = true;
-          }
-        }
-      }
-    }
-  }
-  // scores of the chunk's columns, history POIs excluded, offered to each user's running top-k
-  int nan = 0;
-#pragma unroll
-  for (int i = 0; i < UPW; ++i) {
-    const int64_t slot = gw + int64_t(i) * nwaves;
-    if (i < upw && slot < nusers) {
-    const int32_t hl = __builtin_amdgcn_readlane(my_hl, i);
-    unsigned long long key = 0ull;
-    bool cand = lane < cols && !((hmask >> i) & 1u);
-    if (cand) {
-      float logit = 0.f;   // empty history: logit 0
-      if (hl > 0) logit = acc[i].y / ((beta == 0.5f) ? sqrtf(acc[i].x) : powf(acc[i].x, beta));
-      float sc = 1.0f / (1.0f + expf(-logit));
-      if (logit != logit) {
-        sc = __builtin_nanf("");
-        ++nan;
-      }
-      key = ((unsigned long long)ord_f32_p(sc) << 32) |
-            (unsigned long long)(0xFFFFFFFFu - (uint32_t)(col0 + lane));
-    }
-    const int cnt = kcount[slot];
-    const unsigned long long thr = cnt == k ? keys[slot * k + k - 1] : 0ull;   // valid keys are > 0
-    const unsigned long long offer = __ballot(cand && key > thr);
-    if (offer != 0ull) {
-    unsigned long long* L = lk[w];
-    for (int q = lane; q < cnt; q += 64) L[q] = keys[slot * k + q];
-    const int m = __popcll(offer);
-    if (cand && key > thr) L[cnt + __popcll(offer & ((1ull << lane) - 1ull))] = key;
-    const int n = cnt + m;
-    int n2 = 64;
-    while (n2 < n) n2 <<= 1;
-    for (int q = n + lane; q < n2; q += 64) L[q] = 0ull;
-    wave_lds_sync();
-    for (int size = 2; size <= n2; size <<= 1) {   // bitonic sort, descending
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int q = lane; q < n2; q += 64) {
-          const int partner = q ^ stride;
-          if (partner > q) {
-            const bool desc = (q & size) == 0;
-            const unsigned long long a = L[q], b = L[partner];
-            if (desc ? (a < b) : (a > b)) {
-              L[q] = b;
-              L[partner] = a;
-            }
-          }
-        }
-        wave_lds_sync();
-      }
-    }
-    const int nk = n < k ? n : k;
-    for (int q = lane; q < nk; q += 64) keys[slot * k + q] = L[q];
-    if (lane == 0) kcount[slot] = nk;
-    wave_lds_sync();
-    }
-    }
-  }
-  if (nan_count) {
-    for (int o = 32; o > 0; o >>= 1) nan += __shfl_xor(nan, o);
-    if (lane == 0 && nan) atomicAdd(nan_count, nan);
-  }
 }
 
 
@@ -795,43 +588,6 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
                        std::min<int64_t>(STRIPE, cols - s0), beta, (int)k,
                        reinterpret_cast<unsigned long long*>(keys), kcount, nan_count);
     const int32_t rc = nais_internal_check_launch("pair_gather_topk_kernel");
-    if (rc) return rc;
-  }
-  return NAIS_OK;
-}
-
-int32_t nais_pair_gather_topk_l2(const float* table, int64_t chunk_stride, int64_t num_rows,
-                                 const int32_t* rowmap, const int64_t* indptr, const int64_t* indices,
-                                 const int32_t* users, int32_t num_users, int64_t col0, int64_t cols,
-                                 float beta, int32_t k, uint64_t* keys, int32_t* kcount,
-                                 int32_t* nan_count, int32_t rows_per_block, int32_t max_waves,
-                                 void* stream) {
-  if (num_users < 0 || col0 < 0 || cols < 0 || k <= 0 || num_rows < 0 || rows_per_block <= 0)
-    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
-  if (k > 256) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
-  if (col0 + cols > 0xFFFFFFFFll || num_rows > 0x7ffffffell)
-    return nais_internal_fail(NAIS_E_UNSUPPORTED, "POI ids and rows must fit 32 bits");
-  if (num_users == 0 || cols == 0) return NAIS_OK;
-  if (!table || !rowmap || !indptr || !indices || !users || !keys || !kcount)
-    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
-  if (chunk_stride < num_rows * 128) return nais_internal_fail(NAIS_E_INVALID, "chunk_stride < num_rows * 128");
-  if (chunk_stride % 2 != 0) return nais_internal_fail(NAIS_E_INVALID, "chunk_stride must be even (float2 loads)");
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // users per wave: enough waves to be resident together (max_waves), at most L2_UPW per wave
-  // (more users than max_waves * L2_UPW: the later waves start as the first ones retire, a few
-  // row blocks behind them)
-  const int64_t mw = std::max<int64_t>(1, max_waves);
-  const int upw = int(std::min<int64_t>(L2_UPW, (num_users + mw - 1) / mw));
-  const int nwaves = int((num_users + upw - 1) / upw);
-  const unsigned grid = unsigned((nwaves + L2_WAVES - 1) / L2_WAVES);
-  for (int64_t x0 = 0; x0 < cols; x0 += 64) {    // one launch per chunk: one writer per list
-    const float* T = table + (x0 / 64) * chunk_stride;
-    const int32_t w = int32_t(std::min<int64_t>(64, cols - x0));
-    hipLaunchKernelGGL(pair_gather_topk_l2_kernel<L2_UPW>, dim3(grid), dim3(L2_WAVES * 64), 0, st, T,
-                       num_rows, rows_per_block, rowmap, indptr, indices, users, num_users, upw,
-                       nwaves, col0 + x0, w, beta, (int)k,
-                       reinterpret_cast<unsigned long long*>(keys), kcount, nan_count);
-    const int32_t rc = nais_internal_check_launch("pair_gather_topk_l2_kernel");
     if (rc) return rc;
   }
   return NAIS_OK;

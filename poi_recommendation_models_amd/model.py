@@ -99,10 +99,6 @@ class _NAISDevice(nn.Module):
         _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor),
                                         _capi.ptr(llm), e, es, ld, stream), "nais_pair_table")
 
-    def _pair_table_il(self, lib, prm, items, J, c0, w, reg, cor, llm, table, chunk_stride, stream):
-        _capi.check(lib.nais_pair_table_il(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor),
-                                           _capi.ptr(llm), table, chunk_stride, stream), "nais_pair_table_il")
-
     def _pair_fixup(self, csr, users, m, scores, c0, c1, stream):
         pass
 

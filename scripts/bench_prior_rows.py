@@ -1,7 +1,5 @@
 """Time nais_powerlaw_prior (the per-user prior_kernel, powerLaw.py:90-92) on a config-4-shaped
-slice: U users x 100k POIs, h ~ U{1..200}, (a, b) = bench.py's prior. Prints one JSON line.
-Run twice, with NAIS_PRIOR_EXIT=0 and without, for the underflow-exit A/B (the switch is read once
-per process)."""
+slice: U users x 100k POIs, h ~ U{1..200}, (a, b) = bench.py's prior. Prints one JSON line."""
 import argparse
 import json
 import os
@@ -37,7 +35,7 @@ def main():
         ms.append(t0.elapsed_time(t1))
     zero = float(((G == 0) | (G == -1)).double().mean())
     print(json.dumps({"kernel": "prior_kernel", "users": a.users, "pois": a.pois, "h_max": a.h_max,
-                      "exit": os.environ.get("NAIS_PRIOR_EXIT", "1"), "ms": ms, "best_ms": min(ms),
+                      "ms": ms, "best_ms": min(ms),
                       "pairs_per_s": a.users * a.pois / (min(ms) / 1e3), "frac_zero_or_hist": zero,
                       "checksum_bits": int(G.view(torch.int64).sum().item())}))
 

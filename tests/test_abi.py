@@ -31,6 +31,9 @@ def test_exports_match_header(lib):
                          text=True).stdout
     exported = set(re.findall(r" T (nais_\w+)", out))
     assert set(names) <= exported, set(names) - exported
+    # and nothing beyond the header: no A/B entry points left in the product library
+    internal = {"nais_internal_fail", "nais_internal_check_launch"}
+    assert exported - internal == set(names), exported - internal - set(names)
     for n in names:
         assert hasattr(lib, n)
 

@@ -565,11 +565,6 @@ def test_pairs_auto_choice_and_new4():
     {"PAIR_LPT_ORDER": False, "PAIR_FUSED_TOPK": False},
     {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.1},   # tail users on the table stream
     {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.9, "PAIR_LPT_ORDER": False},
-    {"PAIR_L2_GATHER": True},                                   # L2-blocked gather (interleaved table)
-    {"PAIR_L2_GATHER": True, "PAIR_TABLE_CUS": 0},
-    {"PAIR_L2_GATHER": True, "PAIR_L2_ROWS": 1},                # one row per block
-    {"PAIR_L2_GATHER": True, "PAIR_L2_ROWS": 37, "PAIR_L2_WAVES_PER_CU": 0},   # 16 users per wave
-    {"PAIR_L2_GATHER": True, "PAIR_L2_ROWS": 1 << 20, "PAIR_L2_WAVES_PER_CU": 0},   # one block
 ])
 def test_pairs_blocks_passes_bit_identical(knobs):
     """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, the

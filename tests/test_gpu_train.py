@@ -464,13 +464,15 @@ def test_fused_step_config3_full_catalog(D, H, wd):
     tr = _trainer(m, X, lr=0.02, weight_decay=wd)
     ref = {k: v.copy() for k, v in p.items()}
     st = {k: np.zeros_like(v) for k, v in ref.items()}
+    total = 0.0
     for step in (1, 2):
         hist, data, labels = _batch(P, n, 4, seed=40 + step)
         assert hist.shape == (1020, 204)
         seed = 777 + step
         tr.step(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV),
                 torch.as_tensor(labels).to(DEV), dropout_seed=seed)
-        loss = tr.finish()
+        loss = tr.finish() - total      # finish() returns the running sum of run.py:107
+        total += loss
         keep = _mask(seed, len(data), n, H, 0.5)
         r = train_oracle.train_step_basic(ref, hist, data, labels, keep=keep, drop_p=0.5)
         assert abs(loss - r["loss"]) <= 1e-5, (step, loss, r["loss"])
