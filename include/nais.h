@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 8
+#define NAIS_ABI_VERSION 9
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -533,7 +533,7 @@ typedef struct nais_adagrad_state {
   float* sum_w2;
   float* grad_embed_history;               /* [P, D] zero-maintained gradient scratch              */
   float* grad_embed_target;                /* [P, D]                                               */
-  float* grad_small;                       /* [H*D + 2H]: w1 | b1 | w2                             */
+  float* grad_small;                       /* [H*din + 2H]: w1 | b1 | w2                           */
   int32_t* stamp_embed_history;            /* [P] row-claim stamps, initialised to 0               */
   int32_t* stamp_embed_target;             /* [P]                                                  */
 } nais_adagrad_state_t;
@@ -545,6 +545,32 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
                         int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
                         int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
                         void* stream);
+
+/*
+ * The same fused step for the region / distance variants (run.py:139-200 NAIS_regionEmbedding,
+ * :206-262 NAIS_region_distance_Embedding, :365-430 NAIS_distance_Embedding; batches from
+ * get_NAIS_batch_region, batches.py:67-108): side = the batch's region ids / target_lat_long as
+ * for nais_train_forward_ex (its ucache fields are ignored: the step keeps its own in the
+ * workspace). opt covers embed_history / embed_target (rows of item_dim floats), attn_layer1 (its
+ * grad_small block is [hidden * din | hidden | hidden]) and attn_layer2; opt_side the variant's
+ * extra parameters, updated densely (torch.optim.Adagrad over model.parameters(), run.py:155):
+ * embed_region [num_regions, region_dim] and / or dist_layer (weight [2, 2], bias [2]), each with
+ * a zero-maintained gradient scratch. NAIS_basic with side = opt_side = NULL is nais_train_step.
+ */
+typedef struct nais_adagrad_side {
+  float* sum_embed_region;                 /* [num_regions, region_dim] (region variants)          */
+  float* grad_embed_region;                /* same shape, zero-maintained                          */
+  float* sum_dist_w;                       /* [4] (distance variants)                              */
+  float* sum_dist_b;                       /* [2]                                                  */
+  float* grad_dist;                        /* [6]: dist_w | dist_b, zero-maintained                */
+} nais_adagrad_side_t;
+
+int32_t nais_train_step_ex(const nais_params_t* params, const nais_train_side_t* side,
+                           const nais_adagrad_state_t* opt, const nais_adagrad_side_t* opt_side,
+                           const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
+                           int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
+                           int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
+                           void* stream);
 
 /*
  * get_NAIS_batch (batches.py:24-50) for one user on the device: hist [n] = the

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
@@ -23,7 +23,7 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_score_topk", "nais_score_catalog", "nais_topk_rows", "nais_powerlaw_prior",
            "nais_distance_histogram", "nais_gather_rows", "nais_train_workspace_size",
            "nais_train_forward", "nais_train_backward", "nais_dropout_mask", "nais_adagrad",
-           "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step",
+           "nais_adagrad_rows", "nais_train_step_workspace_size", "nais_train_step", "nais_train_step_ex",
            "nais_make_train_batch", "nais_new4_tables", "nais_pair_rows_workspace_size",
            "nais_pair_rows", "nais_pair_table", "nais_pair_gather", "nais_stream_create_cu_mask",
            "nais_stream_destroy", "nais_near_attention", "nais_copy_columns",
@@ -91,6 +91,12 @@ class NaisAdagradState(ctypes.Structure):
                                         "grad_small", "stamp_embed_history", "stamp_embed_target")]
 
 
+class NaisAdagradSide(ctypes.Structure):
+    """Mirror of `nais_adagrad_side_t` (the region / distance variants' extra Adagrad state)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("sum_embed_region", "grad_embed_region", "sum_dist_w",
+                                               "sum_dist_b", "grad_dist")]
+
+
 class NaisError(RuntimeError):
     pass
 
@@ -156,6 +162,10 @@ def load(path: str | None = None):
     lib.nais_train_step.restype = i32
     lib.nais_train_step.argtypes = [ctypes.POINTER(NaisParams), ctypes.POINTER(NaisAdagradState), vp,
                                     i64, vp, vp, i64, f32, u64, vp, vp, vp, vp, sz, vp]
+    lib.nais_train_step_ex.restype = i32
+    lib.nais_train_step_ex.argtypes = [ctypes.POINTER(NaisParams), ctypes.POINTER(NaisTrainSide),
+                                       ctypes.POINTER(NaisAdagradState), ctypes.POINTER(NaisAdagradSide),
+                                       vp, i64, vp, vp, i64, f32, u64, vp, vp, vp, vp, sz, vp]
     lib.nais_make_train_batch.restype = i32
     lib.nais_make_train_batch.argtypes = [vp, vp, i64, i64, i64, i32, u64, vp, vp, vp, vp, vp]
     lib.nais_new4_tables.restype = i32

@@ -133,19 +133,36 @@ constexpr int STRIPE = 64 * CPL;             // columns per wave
 // while the adds stay in history (CSR) order.
 constexpr int GU = 8;
 
+// CPL columns of one table row for a lane with nv valid columns (CPL: one vector load; fewer, the
+// last lane of a block whose width is not a multiple of CPL: scalar loads, 0 past the block).
+template <typename V, typename T>
+__device__ __forceinline__ V load_cols(const T* __restrict__ p, int nv) {
+  if (nv == CPL) return *reinterpret_cast<const V*>(p);
+  V v;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) v[q] = q < nv ? p[q] : T(0);
+  return v;
+}
+
 // Sa += Σ E[row(j), x..x+CPL), Na += Σ ES[...] over the jn (wave-uniform) rows whose offsets the
-// lanes 0..jn-1 hold in (mlo, mhi), in lane order. Full CPL-column vectors only.
-__device__ __forceinline__ void gather_rows_full(const float* __restrict__ E, const float* __restrict__ ES,
-                                                 uint32_t mlo, uint32_t mhi, int jn, int64_t x,
-                                                 float (&Sa)[CPL], float (&Na)[CPL]) {
+// lanes 0..jn-1 hold in (mlo, mhi), in lane order; nv = this lane's valid columns (0..CPL; past
+// them the sums get +0). Every readlane runs with the whole wave active: a readlane inside a
+// branch on nv could read a lane's register after that lane's side of the branch reused it (the
+// register allocator only keeps values live for the lanes a branch runs), which gave the last
+// lane of an odd-width block wrong rows.
+__device__ __forceinline__ void gather_rows(const float* __restrict__ E, const float* __restrict__ ES,
+                                            uint32_t mlo, uint32_t mhi, int jn, int64_t x, int nv,
+                                            float (&Sa)[CPL], float (&Na)[CPL]) {
   int jj = 0;
   for (; jj + GU <= jn; jj += GU) {
+    int64_t o[GU];
+#pragma unroll
+    for (int g = 0; g < GU; ++g) o[g] = bcast64(mlo, mhi, jj + g) + x;
     nfv e[GU], t[GU];
 #pragma unroll
     for (int g = 0; g < GU; ++g) {
-      const int64_t o = bcast64(mlo, mhi, jj + g) + x;
-      e[g] = loadv(E + o);
-      t[g] = loadv(ES + o);
+      e[g] = load_cols<nfv>(E + o[g], nv);
+      t[g] = load_cols<nfv>(ES + o[g], nv);
     }
 #pragma unroll
     for (int g = 0; g < GU; ++g)
@@ -157,14 +174,18 @@ __device__ __forceinline__ void gather_rows_full(const float* __restrict__ E, co
   }
   for (; jj < jn; ++jj) {
     const int64_t o = bcast64(mlo, mhi, jj) + x;
-    const nfv e = loadv(E + o);
-    const nfv t = loadv(ES + o);
+    const nfv e = load_cols<nfv>(E + o, nv);
+    const nfv t = load_cols<nfv>(ES + o, nv);
 #pragma unroll
     for (int q = 0; q < CPL; ++q) {
       Sa[q] += e[q];
       Na[q] += t[q];
     }
   }
+}
+
+__device__ __forceinline__ int valid_cols(int64_t x, int64_t cols) {
+  return x >= cols ? 0 : (x + CPL <= cols ? CPL : int(cols - x));
 }
 
 __global__ void __launch_bounds__(GW * 64)
@@ -180,7 +201,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
   const int64_t u = users[slot];
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int64_t x = int64_t(blockIdx.y) * STRIPE + lane * CPL;   // column within the block
-  const bool full = x + CPL <= cols;
+  const int nv = valid_cols(x, cols);
   float Sa[CPL], Na[CPL];
 #pragma unroll
   for (int q = 0; q < CPL; ++q) Sa[q] = Na[q] = 0.f;
@@ -189,16 +210,7 @@ pair_gather_kernel(const float* __restrict__ E, const float* __restrict__ ES, in
     // row offsets of 64 history items, one per lane, broadcast with readlane below
     const int64_t mine = lane < jn ? int64_t(rowmap[indices[hb + j0 + lane]]) * ld : 0;
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
-    if (full) {
-      gather_rows_full(E, ES, mlo, mhi, jn, x, Sa, Na);
-    } else {
-      for (int jj = 0; jj < jn; ++jj) {
-        const int64_t o = bcast64(mlo, mhi, jj) + x;
-#pragma unroll
-        for (int q = 0; q < CPL - 1; ++q)
-          if (x + q < cols) { Sa[q] += E[o + q]; Na[q] += ES[o + q]; }
-      }
-    }
+    gather_rows(E, ES, mlo, mhi, jn, x, nv, Sa, Na);
   }
   float* out = scores + slot * score_ld + (col0 - score_col0) + x;
   int nan = 0;
@@ -271,7 +283,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
   const int64_t u = users[slot];
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int64_t x = int64_t(lane) * CPL;     // column within the stripe [col0, col0 + cols)
-  const bool full = x + CPL <= cols;
+  const int nv = valid_cols(x, cols);
   if (lane < STRIPE / 32) hm[w][lane] = 0u;
   wave_lds_sync();
   float Sa[CPL], Na[CPL];
@@ -287,16 +299,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
       if (r >= 0 && r < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
     }
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
-    if (full) {
-      gather_rows_full(E, ES, mlo, mhi, jn, x, Sa, Na);
-    } else {
-      for (int jj = 0; jj < jn; ++jj) {
-        const int64_t o = bcast64(mlo, mhi, jj) + x;
-#pragma unroll
-        for (int q = 0; q < CPL - 1; ++q)
-          if (x + q < cols) { Sa[q] += E[o + q]; Na[q] += ES[o + q]; }
-      }
-    }
+    gather_rows(E, ES, mlo, mhi, jn, x, nv, Sa, Na);
   }
   wave_lds_sync();
   // the wave's candidates and the current k-th key
@@ -420,7 +423,7 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int64_t s0 = int64_t(blockIdx.y) * STRIPE;          // this wave's stripe in the block
   const int64_t x = s0 + int64_t(lane) * CPL;
-  const bool full = x + CPL <= cols;
+  const int nv = valid_cols(x, cols);
   if (lane < STRIPE / 32) hm[w][lane] = 0u;
   wave_lds_sync();
   double g[CPL];
@@ -436,36 +439,37 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
       const int64_t r = c - col0 - s0;
       if (r >= 0 && r < STRIPE && r + s0 < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
     }
-    if (all_zero) continue;   // only the bitmap is left to build
+    if (all_zero) continue;   // only the bitmap is left to build (wave-uniform)
     const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
     int jj = 0;
-    if (full) {   // GU rows' loads in flight (as gather_rows_full), products still in CSR order
-      for (; jj + GU <= jn; jj += GU) {
-        ndv rv[GU];
+    // GU rows' loads in flight (as gather_rows), products still in CSR order; readlanes and the
+    // ballot with the whole wave active (columns past the block hold 0.0 and stay 0.0)
+    for (; jj + GU <= jn; jj += GU) {
+      int64_t o[GU];
 #pragma unroll
-        for (int u2 = 0; u2 < GU; ++u2)
-          rv[u2] = *reinterpret_cast<const ndv*>(pr + bcast64(mlo, mhi, jj + u2) + x);
+      for (int u2 = 0; u2 < GU; ++u2) o[u2] = bcast64(mlo, mhi, jj + u2) + x;
+      ndv rv[GU];
 #pragma unroll
-        for (int u2 = 0; u2 < GU; ++u2)
+      for (int u2 = 0; u2 < GU; ++u2) rv[u2] = load_cols<ndv>(pr + o[u2], nv);
 #pragma unroll
-          for (int q = 0; q < CPL; ++q) g[q] = __dmul_rn(g[q], rv[u2][q]);
-        if (zero_exit) {
-          bool nz = false;
+      for (int u2 = 0; u2 < GU; ++u2)
 #pragma unroll
-          for (int q = 0; q < CPL; ++q) nz |= g[q] != 0.0;
-          if (__ballot(nz) == 0ull) {
-            all_zero = true;
-            break;
-          }
+        for (int q = 0; q < CPL; ++q) g[q] = __dmul_rn(g[q], rv[u2][q]);
+      if (zero_exit) {
+        bool nz = false;
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) nz |= g[q] != 0.0;
+        if (__ballot(nz) == 0ull) {
+          all_zero = true;
+          break;
         }
       }
     }
     if (all_zero) continue;
     for (; jj < jn; ++jj) {
-      const double* row = pr + bcast64(mlo, mhi, jj) + x;
+      const ndv rv = load_cols<ndv>(pr + bcast64(mlo, mhi, jj) + x, nv);
 #pragma unroll
-      for (int q = 0; q < CPL; ++q)
-        if (x + q < cols) g[q] = __dmul_rn(g[q], row[q]);
+      for (int q = 0; q < CPL; ++q) g[q] = __dmul_rn(g[q], rv[q]);
     }
     if (zero_exit) {
       bool nz = false;

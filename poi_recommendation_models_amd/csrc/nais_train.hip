@@ -691,18 +691,19 @@ __device__ __forceinline__ void adagrad_elem(float* p, float* st, float* g, floa
   *g = 0.f;
 }
 
-__global__ void step_adagrad_kernel(StepOpt o, int H, int D, const int64_t* __restrict__ hist,
+// DIN = attn_layer1's input width (the w1 block of g_small is H x DIN), D = the embedding rows' width
+__global__ void step_adagrad_kernel(StepOpt o, int H, int DIN, int D, const int64_t* __restrict__ hist,
                                     int64_t n, const int64_t* __restrict__ target, int64_t b,
                                     int64_t dense_rows, const int32_t* __restrict__ bad_rows) {
   if (*bad_rows) return;
-  const int64_t wsz = int64_t(H) * D + 2 * H;
+  const int64_t wsz = int64_t(H) * DIN + 2 * H;
   const int64_t nsmall_blocks = (wsz + 255) / 256;
   const int64_t bx = blockIdx.x;
   if (bx < nsmall_blocks) {
     const int64_t e = bx * 256 + threadIdx.x;
     if (e < wsz) {
-      const int k = e < int64_t(H) * D ? 0 : (e < int64_t(H) * D + H ? 1 : 2);
-      const int64_t off = k == 0 ? e : (k == 1 ? e - int64_t(H) * D : e - int64_t(H) * D - H);
+      const int k = e < int64_t(H) * DIN ? 0 : (e < int64_t(H) * DIN + H ? 1 : 2);
+      const int64_t off = k == 0 ? e : (k == 1 ? e - int64_t(H) * DIN : e - int64_t(H) * DIN - H);
       adagrad_elem(o.p_small[k] + off, o.s_small[k] + off, o.g_small + e, o.clr, o.wd, o.eps);
     }
     return;
@@ -733,6 +734,17 @@ __global__ void step_adagrad_kernel(StepOpt o, int H, int D, const int64_t* __re
       else adagrad_elem(o.p_eh + i, o.s_eh + i, o.g_eh + i, o.clr, 0.f, o.eps);
     }
   }
+}
+
+// Adagrad of a whole small tensor from its zero-maintained gradient scratch (the fused step of the
+// region variants: embed_region, every row -- the region ids of a batch are few, and a row whose
+// gradient is 0 is left bit-identical with weight_decay 0 -- and dist_layer's weight / bias).
+__global__ void step_adagrad_dense_kernel(float* p, float* st, float* g, int64_t numel, float clr,
+                                          float wd, float eps, const int32_t* __restrict__ bad_rows) {
+  if (*bad_rows) return;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < numel;
+       e += int64_t(gridDim.x) * blockDim.x)
+    adagrad_elem(p + e, st + e, g + e, clr, wd, eps);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1741,17 +1753,26 @@ size_t nais_train_step_workspace_size(const nais_params_t* params, int64_t b, in
            : nais_train_workspace_size(params, b, n) + size_t(4 * b) * sizeof(float);
 }
 
-int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
+namespace {
+int32_t train_step_impl(const nais_params_t* params, const nais_train_side_t* side,
+                        const nais_adagrad_state_t* opt, const nais_adagrad_side_t* opt_side,
                         const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
                         int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
                         int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
                         void* stream) {
   TShape sh{0, 0};
   const bool fast = params && fast_ok(params);
-  int rc = fast ? tvalidate(params, &sh) : gvalidate(params, nullptr, b, n);
+  int rc = fast ? tvalidate(params, &sh) : gvalidate(params, side, b, n);
   if (rc) return rc;
-  if (params->variant != NAIS_VARIANT_BASIC)
-    return nais_internal_fail(NAIS_E_UNSUPPORTED, "nais_train_step: NAIS_basic only (use nais_train_*_ex)");
+  const bool region = params->variant == NAIS_VARIANT_REGION ||
+                      params->variant == NAIS_VARIANT_REGION_DISTANCE;
+  const bool distv = params->variant == NAIS_VARIANT_REGION_DISTANCE ||
+                     params->variant == NAIS_VARIANT_DISTANCE;
+  if ((region || distv) &&
+      (!opt_side || (region && (!opt_side->sum_embed_region || !opt_side->grad_embed_region)) ||
+       (distv && (!opt_side->sum_dist_w || !opt_side->sum_dist_b || !opt_side->grad_dist))))
+    return nais_internal_fail(NAIS_E_INVALID, "nais_adagrad_side_t: missing buffer for the variant's "
+                                              "embed_region / dist_layer");
   if ((rc = check_batch(hist, n, target, b))) return rc;
   if (!(dropout_p >= 0.f && dropout_p <= 1.f))
     return nais_internal_fail(NAIS_E_INVALID, "dropout_p must be in [0, 1]");
@@ -1772,7 +1793,8 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
   float* own_pred = ws + 3 * b; // [b]
   float* part = ws + 4 * b;     // forward partials, then backward partials
   if (!pred) pred = own_pred;
-  const int D = params->embed_dim, H = params->hidden;
+  const int D = params->embed_dim, H = params->hidden, DIN = params->din;
+  const int RD = region ? params->item_dim : D;   // embed_history / embed_target row width
   int64_t ns = 0, rb = (b + TROWS - 1) / TROWS;
   int js = 1;
   GArgs ga{};
@@ -1780,7 +1802,7 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
     if (fast) {
       js = slice_items(b, n, FWD_PER_CU);
     } else {
-      ga = gargs(params, nullptr, hist, n, target, b, dropout_p, seed);
+      ga = gargs(params, side, hist, n, target, b, dropout_p, seed);
       js = ga.js;
       if (step_ucache_bytes(params, b, n))
         ga.ucache = reinterpret_cast<float*>(static_cast<char*>(workspace) +
@@ -1806,8 +1828,10 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
   // 3. backward partials, 4. reduce into the zero-maintained gradient scratch
   if (n > 0 && !fast) {   // general kernels add straight into the scratch
     float* gs = opt->grad_small;
-    const GGrads g{opt->grad_embed_history, opt->grad_embed_target, nullptr, gs,
-                   gs + int64_t(H) * D, gs + int64_t(H) * D + H, nullptr, nullptr};
+    float* gd = distv ? opt_side->grad_dist : nullptr;
+    const GGrads g{opt->grad_embed_history, opt->grad_embed_target,
+                   region ? opt_side->grad_embed_region : nullptr, gs, gs + int64_t(H) * DIN,
+                   gs + int64_t(H) * DIN + H, gd, gd ? gd + 4 : nullptr};
     if ((rc = g_backward(ga, saved, pred, gpred, g, st, bad_rows))) return rc;
   } else if (n > 0) {
     float* Wt = part;
@@ -1844,13 +1868,53 @@ int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t*
   o.wd = opt->weight_decay;
   o.eps = opt->eps;
   o.tag = int32_t(opt->step);
-  const int64_t wsz = int64_t(H) * D + 2 * H;
+  const int64_t wsz = int64_t(H) * DIN + 2 * H;
   const int64_t dense = opt->weight_decay != 0.f ? params->num_pois : 0;
   const int64_t rows = dense ? 2 * dense : n + b;
   const int64_t blocks = (wsz + 255) / 256 + (rows + 3) / 4;
-  hipLaunchKernelGGL(step_adagrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, o, H, D, hist,
-                     n, target, b, dense, bad_rows);
-  return nais_internal_check_launch("step_adagrad_kernel");
+  hipLaunchKernelGGL(step_adagrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, o, H, DIN, RD,
+                     hist, n, target, b, dense, bad_rows);
+  if ((rc = nais_internal_check_launch("step_adagrad_kernel"))) return rc;
+  if (region) {   // every row of embed_region (its batch rows are a few region ids)
+    const int64_t ne = int64_t(params->num_regions) * params->region_dim;
+    hipLaunchKernelGGL(step_adagrad_dense_kernel, dim3((unsigned)std::min<int64_t>((ne + 255) / 256, 1024)),
+                       dim3(256), 0, st, const_cast<float*>(params->embed_region),
+                       opt_side->sum_embed_region, opt_side->grad_embed_region, ne, o.clr, o.wd, o.eps,
+                       bad_rows);
+    if ((rc = nais_internal_check_launch("step_adagrad_dense_kernel"))) return rc;
+  }
+  if (distv) {    // dist_layer weight [2, 2] and bias [2]
+    hipLaunchKernelGGL(step_adagrad_dense_kernel, dim3(1), dim3(64), 0, st,
+                       const_cast<float*>(params->dist_w), opt_side->sum_dist_w, opt_side->grad_dist,
+                       int64_t(4), o.clr, o.wd, o.eps, bad_rows);
+    hipLaunchKernelGGL(step_adagrad_dense_kernel, dim3(1), dim3(64), 0, st,
+                       const_cast<float*>(params->dist_b), opt_side->sum_dist_b, opt_side->grad_dist + 4,
+                       int64_t(2), o.clr, o.wd, o.eps, bad_rows);
+    if ((rc = nais_internal_check_launch("step_adagrad_dense_kernel"))) return rc;
+  }
+  return NAIS_OK;
+}
+}  // namespace
+
+int32_t nais_train_step(const nais_params_t* params, const nais_adagrad_state_t* opt,
+                        const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
+                        int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
+                        int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+  if (params && params->variant != NAIS_VARIANT_BASIC)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "nais_train_step: NAIS_basic only (use nais_train_step_ex)");
+  return train_step_impl(params, nullptr, opt, nullptr, hist, n, target, labels, b, dropout_p, seed,
+                         loss_sum, bad_rows, pred, workspace, workspace_bytes, stream);
+}
+
+int32_t nais_train_step_ex(const nais_params_t* params, const nais_train_side_t* side,
+                           const nais_adagrad_state_t* opt, const nais_adagrad_side_t* opt_side,
+                           const int64_t* hist, int64_t n, const int64_t* target, const float* labels,
+                           int64_t b, float dropout_p, uint64_t seed, float* loss_sum,
+                           int32_t* bad_rows, float* pred, void* workspace, size_t workspace_bytes,
+                           void* stream) {
+  return train_step_impl(params, side, opt, opt_side, hist, n, target, labels, b, dropout_p, seed,
+                         loss_sum, bad_rows, pred, workspace, workspace_bytes, stream);
 }
 
 int32_t nais_make_train_batch(const int64_t* indptr, const int64_t* indices, int64_t user,

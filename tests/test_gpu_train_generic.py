@@ -191,3 +191,120 @@ def test_train_generic_errors():
     m = M.NAIS_basic(100, 256, 16, 0.5).to(DEV).train()   # embed_dim > 128
     with pytest.raises(RuntimeError, match="128"):
         m(_t(np.zeros((3, 2), np.int64)), _t(np.arange(3)))
+
+
+# ------------------------------------------------ device-side region / distance training (f1 + f2)
+def _csr_region(U, P, h_max, seed, h_min=2):
+    import scipy.sparse as sp
+    r = np.random.default_rng(seed)
+    rows, cols = [], []
+    for u in range(U):
+        h = int(r.integers(h_min, h_max + 1))
+        rows += [u] * h
+        cols += sorted(r.choice(P, h, replace=False).tolist())
+    return sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(U, P))
+
+
+@pytest.mark.parametrize("case,D,H,drop,wd", [
+    ("region", 64, 64, 0.5, 0.0),
+    ("region", 128, 128, 0.5, 0.01),
+    ("region_distance", 64, 48, 0.0, 0.0),
+    ("region_distance", 128, 128, 0.0, 0.01),
+    ("distance", 64, 64, 0.0, 0.0),
+])
+def test_trainer_region_step_oracle(case, D, H, drop, wd):
+    """NAISTrainer drives the region / distance variants on the device --
+    get_NAIS_batch_region's region ids (batches.py:67-108) and run.py:240-245's target_lat_long built
+    from the CSR, region_of and the POI coordinates by nais_make_train_batch + device gathers, one
+    nais_train_step_ex per step (forward, BCELoss, backward, torch.optim.Adagrad over every
+    parameter, embed_region / dist_layer densely). Two steps against oracle/train_oracle.py carried
+    over both: the batch the device drew is read back and fed to the oracle, dropout with the
+    device's mask injected; loss within 1e-5, every updated parameter within rtol 1e-4."""
+    from poi_recommendation_models_amd.trainer import NAISTrainer
+    P, R = 3000, 40
+    p = _params(case, P, R, D, H, seed=D + H + 7)
+    X = _csr_region(6, P, 40, seed=D + H)
+    r = np.random.default_rng(3)
+    region_of = r.integers(0, R, P)
+    coords = np.stack([40.7 + r.random(P) * 0.05, -74.0 + r.random(P) * 0.05], 1)
+    if case == "distance":          # a 10x tighter box keeps the x1000 feature off saturation
+        coords = coords.mean(0) + (coords - coords.mean(0)) * 0.1
+    m = _make(case, p, drop)
+    tr = NAISTrainer(m, X, lr=0.02, weight_decay=wd, region_of=region_of, poi_coords=coords)
+    ref = {k: v.copy() for k, v in p.items()}
+    st = {k: np.zeros_like(v) for k, v in p.items()}
+    total = 0.0
+    for step, uid in ((1, 2), (2, 5)):
+        batch = tr.batch(uid, seed=100 + step)
+        hist, data, labels = (t.cpu().numpy() for t in batch[:3])
+        b, n = len(data), len(hist)
+        kw = {}
+        if case != "distance":
+            hreg, dreg = batch[3].cpu().numpy(), batch[4].cpu().numpy()
+            np.testing.assert_array_equal(hreg, region_of[hist])           # batches.py:96-101
+            np.testing.assert_array_equal(dreg, region_of[data])
+            kw.update(hist_region=np.repeat(hreg[None], b, 0), data_region=dreg)
+        if case != "region":
+            ll = batch[-1].cpu().numpy()
+            want = np.abs(coords[data][:, None, :] - coords[hist][None, :, :]).astype(np.float32)
+            np.testing.assert_array_equal(ll, want)                        # run.py:47-54, 240-245
+            kw["latlon"] = ll
+        if case == "distance":
+            kw["dist_scale"] = 1000.0
+        seed = 424242 + step
+        tr.step(*batch, dropout_seed=seed)
+        loss = tr.finish() - total
+        total += loss
+        keep = _mask(seed, b, n, H, drop) if drop > 0 else None
+        o = train_oracle.train_step(ref, np.repeat(hist[None], b, 0), data, labels, keep=keep,
+                                    drop_p=drop, **kw)
+        assert abs(loss - o["loss"]) <= 1e-5, (step, loss, o["loss"])
+        for k in ref:
+            ref[k], st[k] = train_oracle.adagrad(ref[k], st[k], o["grads"][k].reshape(ref[k].shape),
+                                                 0.02, step, weight_decay=wd)
+    got = dict(m.named_parameters())
+    for k in ref:
+        g = got[k].detach().cpu().numpy()
+        bad = ~np.isclose(g, ref[k], rtol=1e-4, atol=2e-5)
+        assert bad.mean() <= 1e-3, (k, int(bad.sum()), bad.size)
+    for k, s in tr.optimizer_state().items():
+        np.testing.assert_allclose(s["sum"].cpu().numpy(), st[k], rtol=1e-3, atol=1e-9)
+    assert not tr._g_small.any() and (tr._g_er is None or not tr._g_er.any())
+    assert tr._g_dist is None or not tr._g_dist.any()
+
+
+@pytest.mark.parametrize("case", ["region", "region_distance"])
+def test_trainer_region_epochs_reduce_loss(case):
+    """run.py:139-200 / 206-262 as NAISTrainer.epoch: every user's device batch and fused step,
+    one host sync per epoch; the summed loss falls."""
+    from poi_recommendation_models_amd.trainer import NAISTrainer
+    P, R, D, H = 2000, 30, 64, 64
+    p = _params(case, P, R, D, H, seed=9)
+    for k in ("embed_history.weight", "embed_target.weight", "embed_region.weight"):
+        if k in p:
+            p[k] = (p[k] * 0.03).astype(np.float32)      # the reference's N(0, 0.01)-like init scale
+    X = _csr_region(40, P, 30, seed=4)
+    r = np.random.default_rng(5)
+    region_of = r.integers(0, R, P)
+    coords = np.stack([40.7 + r.random(P) * 0.05, -74.0 + r.random(P) * 0.05], 1)
+    m = _make(case, p, 0.5 if case == "region" else 0.0)
+    tr = NAISTrainer(m, X, lr=0.05, region_of=region_of, poi_coords=coords)
+    losses = [tr.epoch() for _ in range(6)]
+    assert all(np.isfinite(losses))
+    assert losses[-1] < 0.8 * losses[0], losses
+    assert not tr._g_eh.any() and not tr._g_et.any() and not tr._g_small.any() and not tr._g_er.any()
+
+
+def test_trainer_region_errors():
+    from poi_recommendation_models_amd import model as M
+    from poi_recommendation_models_amd.trainer import NAISTrainer
+    X = _csr_region(3, 100, 5, seed=1)
+    m = M.NAIS_regionEmbedding(100, 32, 16, 0.5, 5).to(DEV).train()
+    with pytest.raises(ValueError, match="region_of"):
+        NAISTrainer(m, X)
+    tr = NAISTrainer(m, X, region_of=np.zeros(100, np.int64))
+    hist, tgt, lab, hreg, treg = tr.batch(0, seed=1)
+    with pytest.raises(TypeError):
+        tr.step(hist, tgt, lab)                      # the region ids are required
+    tr.step(hist, tgt, lab, hreg, treg)
+    assert np.isfinite(tr.finish())
