@@ -1399,6 +1399,360 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 }
 
 // ---------------------------------------------------------------------------------------------
+// The fp16x6 item-side kernel on v_mfma_f32_16x16x32_f16 ("x6n", D in {32, 64}, H <= 64, NAIS_basic
+// and the region variant): the x3b factorisation A_j t_c, the same six products of exact hi / mid /
+// lo f16 pieces, the same per-wave candidate scale and pipelined epilogue, in 16 x 16 output tiles:
+//   A (16 hidden x 32 dims)    lane l: hidden 16 m + (l & 15), dims 32 s + 8 (l >> 4) .. + 8 (LDS ring)
+//   B (32 dims x 16 cands)     lane l: candidate 16 nb + (l & 15), the same dims (VGPRs, 2 blocks nb)
+//   C (16 hidden x 16 cands)   lane l: candidate (l & 15), hidden 16 m + 4 (l >> 4) + r
+// Each A fragment feeds the wave's two candidate blocks. A 16x16x32 MFMA takes half the cycles of
+// a 32x32x16 one for half the work, so the same 1,536 matrix cycles per item and wave; what the
+// shape changes is the clock the chip holds under the load (MI355X_MICROARCH.md, DVFS give-back
+// item 7) and the issue pressure (an MFMA holds the SIMD's vector issue 8 of its 16 cycles instead
+// of 8 of 32). The attention logit of a candidate is summed over the four lane groups by one
+// v_permlane32_swap + one v_permlane16_swap for both candidate blocks at once; s = h_j . t_c comes
+// from a per-chunk s tile (items x candidates) that each wave parks in its own LDS slot in
+// [candidate][item] order, one ds_read per pair.
+// ---------------------------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx4 mfma16n(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// the six fp16x6 products, smallest terms first (as mfma_pieces<3>)
+__device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const half8 (&b)[3], floatx4 c) {
+  c = mfma16n(a[2], b[0], c);
+  c = mfma16n(a[1], b[1], c);
+  c = mfma16n(a[0], b[2], c);
+  c = mfma16n(a[1], b[0], c);
+  c = mfma16n(a[0], b[1], c);
+  c = mfma16n(a[0], b[0], c);
+  return c;
+}
+
+template <int D, int MB>   // D input dims (a multiple of 32), MB blocks of 16 hidden units
+struct CfgN {
+  static constexpr int KS = D / 32;                    // K-steps of 32 dims
+  static constexpr int NE = MB * KS * 64;              // uint4 entries per item and piece
+  static constexpr int IB = NE * 16 * 3;               // LDS bytes per item (three pieces)
+  static constexpr int G = 2;                          // items per ring group (even: two acc sets)
+  static constexpr int JCB = 32;                       // chunk rows (the s tile's items)
+  static constexpr int NW = 8, THREADS = NW * 64, CPB = NW * 32;
+  static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread
+  static constexpr int HP = MB * 16;                   // hidden units, padded
+  static constexpr int EPI = 2 * HP;                   // [b1 | w2] by hidden unit
+  static constexpr int SVP = JCB + 1;                  // s image pitch (floats): [cand][item]
+  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
+                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4;
+};
+
+template <int D, int MB, bool REGION>
+__global__ void __launch_bounds__(512, 1)
+catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
+                         const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
+                         const int64_t* __restrict__ region_of, float* __restrict__ scores,
+                         int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
+  using C = CfgN<D, MB>;
+  constexpr int KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT, HP = C::HP;
+  constexpr int EPI = C::EPI, NW = C::NW, THREADS = C::THREADS, CPB = C::CPB, SVP = C::SVP;
+  constexpr int DH = D / 2;   // region variants: dims [DH, D) come from embed_region
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* ring = reinterpret_cast<uint4*>(smem);                    // [2 groups][G items][piece][NE]
+  float* Eimg = reinterpret_cast<float*>(ring + 2 * G * 3 * NE);   // [b1 | w2] by hidden unit
+  float* Escl = Eimg + EPI;                                        // per wave [S*b1 | w2/S]
+  float* red = Escl + NW * EPI;
+  float* hrows = red + 16;                                         // [JCB][D]
+  int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
+  float* svt = reinterpret_cast<float*>(hid + JCB);                // per wave [32 cands][SVP]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = lane >> 4, l16 = lane & 15;
+  int64_t hbeg, hlen;
+  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
+    hbeg = (int64_t)cat_user_slot() * tab.gi;
+    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  } else {
+    const int64_t u = users[cat_user_slot()];
+    hbeg = indptr[u];
+    hlen = indptr[u + 1] - hbeg;
+  }
+  const int64_t cbase = tab.col0 + (int64_t)cat_tile() * CPB + wave * 32;
+  const int64_t clim = tab.e ? std::min<int64_t>(p.P, tab.col0 + tab.cols) : p.P;
+  // after the lane-group reduction lane L holds candidate cbase + 16 (L >> 5) + (L & 15) (L and
+  // L ^ 16 alike): lane groups 0 / 2 carry e, groups 1 / 3 e * s
+  const int64_t cout = cbase + 16 * (lane >> 5) + l16;
+  const bool vout = cout < clim;
+
+  // ---- this thread's W1 values for its build entries (fp32, unscaled)
+  float wv[EPT][8];
+  float wmax = 0.f;
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * THREADS;
+    const int ln = e & 63, s = (e >> 6) % KS, m = (e >> 6) / KS;
+    const int i = 16 * m + (ln & 15), k0 = 32 * s + 8 * (ln >> 4);
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      wv[q][x] = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
+      wmax = fmaxf(wmax, fabsf(wv[q][x]));
+    }
+  }
+  for (int f = tid; f < EPI; f += THREADS) {
+    const int i = f % HP;
+    Eimg[f] = (i < p.H) ? (f < HP ? p.b1[i] : p.w2[i]) : 0.f;
+  }
+  const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg
+
+  // ---- candidate operands: two blocks of 16, one scale S_t per wave, split into B fragments
+  half8 tb[2][KS][3];
+  float St;
+  {
+    float tv[2][KS][8];
+    float tmax = 0.f;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int64_t c = cbase + 16 * nb + l16;
+      const int64_t cc = c < clim ? c : p.P - 1;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k0 = 32 * s + 8 * grp;
+        const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
+                                                : p.et + cc * p.item_dim + k0;
+        const float4 v0 = reinterpret_cast<const float4*>(src)[0];
+        const float4 v1 = reinterpret_cast<const float4*>(src)[1];
+        tv[nb][s][0] = v0.x; tv[nb][s][1] = v0.y; tv[nb][s][2] = v0.z; tv[nb][s][3] = v0.w;
+        tv[nb][s][4] = v1.x; tv[nb][s][5] = v1.y; tv[nb][s][6] = v1.z; tv[nb][s][7] = v1.w;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) tmax = fmaxf(tmax, fabsf(tv[nb][s][x]));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+    St = pow2_scale(tmax);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = tv[nb][s][e] * St;
+        split_pieces<3>(x, tb[nb][s]);
+      }
+  }
+
+  float S = 0.f, N = 0.f;
+  bool in_hist = false;
+  const float* eb = Escl + wave * EPI;        // S*b1 by hidden unit
+  const float* ew = eb + HP;                  // w2/S
+  float* sv_mine = svt + wave * 32 * SVP;
+  float SAcur = 1.f;
+  int64_t j0 = 0;
+
+  auto build = [&](int jj, int grp_, int it) {   // chunk item jj's fragments into ring slot (grp_, it)
+    const float* hr = hrows + jj * D;
+    uint4* dst = ring + ((grp_ * G + it) * 3) * NE;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * THREADS;
+      if (e < NE) {
+        const int ln = e & 63, s = (e >> 6) % KS;
+        const int k0 = 32 * s + 8 * (ln >> 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
+        const float4 h1 = *reinterpret_cast<const float4*>(hr + k0 + 4);
+        float a[8];
+        a[0] = wv[q][0] * h0.x; a[1] = wv[q][1] * h0.y; a[2] = wv[q][2] * h0.z; a[3] = wv[q][3] * h0.w;
+        a[4] = wv[q][4] * h1.x; a[5] = wv[q][5] * h1.y; a[6] = wv[q][6] * h1.z; a[7] = wv[q][7] * h1.w;
+        half8 pc[3];
+        split_pieces<3>(a, pc);
+#pragma unroll
+        for (int q2 = 0; q2 < 3; ++q2) dst[q2 * NE + e] = *reinterpret_cast<const uint4*>(&pc[q2]);
+      }
+    }
+  };
+
+  // the pair (chunk item pj, this lane's output candidate): the logit partials of the two candidate
+  // blocks summed over the lane groups, then e and e * s
+  auto tail = [&](int pj, float p0, float p1, bool live) {
+    const auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
+    const float q = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);   // groups {g, g + 2}
+    const auto r2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(q), __float_as_uint(q), false, false);
+    const float a = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);   // all four groups
+    const float sv = sv_mine[(16 * (lane >> 5) + l16) * SVP + pj];
+    const bool keep = hid[pj] != (int32_t)cout;
+    const float e = expf(a) * (keep ? 1.f : 0.f);
+    if (live) {
+      if (tab.e) {
+        if (vout) {
+          const int64_t o = (hbeg + j0 + pj) * tab.ld + (cout - tab.col0);
+          if (grp & 1) tab.es[o] = e * sv;
+          else tab.e[o] = e;
+        }
+      } else {
+        in_hist |= !keep;
+        S += e;
+        N += e * sv;
+      }
+    }
+  };
+
+  // item `cur`'s MFMAs (ring slot src) into accN, with the epilogue of item `prev` (accP) cut into
+  // slices between them
+  auto step = [&](auto do_mma, const uint4* src, floatx4 (&accN)[MB][2], const floatx4 (&accP)[MB][2],
+                  int prev, bool live) {
+    constexpr bool MMA = decltype(do_mma)::value;
+    constexpr int NU = KS * MB;                 // (s, m) units of 12 MFMAs
+    constexpr int NV = 2 * MB;                  // epilogue slices: (nb, m), 4 values each
+    constexpr int VPU = (NV + NU - 1) / NU;
+    float ap0 = 0.f, ap1 = 0.f;
+    if (MMA) {
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        const float4 b4 = *reinterpret_cast<const float4*>(eb + 16 * m + 4 * grp);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          accN[m][nb][0] = b4.x; accN[m][nb][1] = b4.y; accN[m][nb][2] = b4.z; accN[m][nb][3] = b4.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int s = u / MB, m = u % MB;
+      if (MMA) {
+        half8 a_[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
+          a_[q] = *reinterpret_cast<const half8*>(&u4);
+        }
+        accN[m][0] = mfma16n_pieces(a_, tb[0][s], accN[m][0]);
+        accN[m][1] = mfma16n_pieces(a_, tb[1][s], accN[m][1]);
+      }
+#pragma unroll
+      for (int v = u * VPU; v < (u + 1) * VPU && v < NV; ++v) {
+        const int nb = v / MB, mm = v % MB;
+        const float4 w4 = *reinterpret_cast<const float4*>(ew + 16 * mm + 4 * grp);
+        float t = nb ? ap1 : ap0;
+        t = __builtin_fmaf(w4.x, relu_bits(accP[mm][nb][0]), t);
+        t = __builtin_fmaf(w4.y, relu_bits(accP[mm][nb][1]), t);
+        t = __builtin_fmaf(w4.z, relu_bits(accP[mm][nb][2]), t);
+        t = __builtin_fmaf(w4.w, relu_bits(accP[mm][nb][3]), t);
+        if (nb) ap1 = t; else ap0 = t;
+      }
+    }
+    tail(prev >= 0 ? prev : 0, ap0, ap1, live);
+  };
+
+  floatx4 acc2[2][MB][2];
+  for (j0 = 0; j0 < hlen; j0 += JCB) {
+    const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
+    __syncthreads();   // the previous chunk's ring, hrows and hid readers are done
+    float hmax = 0.f;
+    for (int f = tid; f < jn * (D / 4); f += THREADS) {
+      const int jj = f / (D / 4), q4 = f % (D / 4);
+      const int64_t item = indices[hbeg + j0 + jj];
+      float4 v;
+      if (!REGION || q4 < DH / 4)
+        v = reinterpret_cast<const float4*>(p.eh + item * p.item_dim)[q4];
+      else
+        v = reinterpret_cast<const float4*>(p.er + region_of[item] * p.region_dim)[q4 - DH / 4];
+      reinterpret_cast<float4*>(hrows)[f] = v;
+      hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int jj = tid; jj < jn; jj += THREADS) hid[jj] = (int32_t)indices[hbeg + j0 + jj];
+    const float Hm = block_max_n<NW>(hmax, red);   // barrier: chunk published
+    const float SA = pow2_scale(Wmax * Hm);
+    const float rs = SA / SAcur;                   // exact power-of-two ratio
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+#pragma unroll
+      for (int x = 0; x < 8; ++x) wv[q][x] *= rs;
+    SAcur = SA;
+    const float Sacc = SA * St, invS = 1.f / Sacc;
+    for (int f = lane; f < EPI; f += 64) Escl[wave * EPI + f] = Eimg[f] * (f < HP ? Sacc : invS);
+    {   // s tile of the chunk: items (pieces of h * S_h, M) x this wave's candidates (N), kept as
+        // s = value / (S_h S_t) in the wave's own LDS slot, [candidate][item]
+      const float Sh = pow2_scale(Hm);
+      const float invShSt = 1.f / (Sh * St);
+      floatx4 sacc[2][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) sacc[mi][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int it = 16 * mi + l16;
+        const bool ok = it < jn;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const float* hp = hrows + it * D + 32 * s + 8 * grp;
+          const float4 h0 = *reinterpret_cast<const float4*>(hp);
+          const float4 h1 = *reinterpret_cast<const float4*>(hp + 4);
+          float x[8];
+          x[0] = ok ? h0.x * Sh : 0.f; x[1] = ok ? h0.y * Sh : 0.f;
+          x[2] = ok ? h0.z * Sh : 0.f; x[3] = ok ? h0.w * Sh : 0.f;
+          x[4] = ok ? h1.x * Sh : 0.f; x[5] = ok ? h1.y * Sh : 0.f;
+          x[6] = ok ? h1.z * Sh : 0.f; x[7] = ok ? h1.w * Sh : 0.f;
+          half8 hpc[3];
+          split_pieces<3>(x, hpc);
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) sacc[mi][nb] = mfma16n_pieces(hpc, tb[nb][s], sacc[mi][nb]);
+        }
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sv_mine[(16 * nb + l16) * SVP + 16 * mi + 4 * grp + r] = sacc[mi][nb][r] * invShSt;
+    }
+    const int ngroups = (jn + G - 1) / G;
+#pragma unroll
+    for (int it = 0; it < G; ++it)
+      if (it < jn) build(it, 0, it);
+    __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
+    int prev = -1;
+    for (int g = 0; g < ngroups; ++g) {
+      if (g + 1 < ngroups) {
+#pragma unroll
+        for (int it = 0; it < G; ++it) {
+          const int jj = (g + 1) * G + it;
+          if (jj < jn) build(jj, (g + 1) & 1, it);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < G; ++it) {
+        const int jj = g * G + it;
+        if (jj < jn) {
+          const uint4* src = ring + (((g & 1) * G + it) * 3) * NE;
+          step(std::true_type{}, src, acc2[it & 1], acc2[(it + 1) & 1], prev, prev >= 0);
+          prev = jj;
+        }
+      }
+      __syncthreads();
+    }
+    if (prev >= 0) {   // drain: the epilogue of the chunk's last item, no MFMAs
+      if (prev & 1)
+        step(std::false_type{}, ring, acc2[0], acc2[1], prev, true);
+      else
+        step(std::false_type{}, ring, acc2[1], acc2[0], prev, true);
+    }
+  }
+  if (tab.e) return;
+
+  const float logit = finish_logit(S, N, p.beta, hlen == 0);
+  const bool isnan_ = logit != logit;
+  float sc = sigmoidf_ref(logit);
+  if (isnan_) sc = __builtin_nanf("");
+  if (in_hist) sc = -1.f;
+  const bool writer = vout && !(grp & 1);
+  if (writer) scores[(int64_t)cat_user_slot() * score_ld + cout] = sc;
+  if (nan_count) {
+    const unsigned long long m = __ballot(writer && !in_hist && isnan_);
+    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Top-k per user (validation.py:26-27): exact radix select on 64-bit keys
 //   key = ordered(score) << 32 | (0xFFFFFFFF - poi)   -> unique; larger key = (higher score, lower id)
 // MSB-first 8-bit passes over the user's score row until the keys at or above the selected prefix
@@ -2087,11 +2441,42 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
   }
 }
 
+// the 16x16x32 item-side kernel instead of x3b for the fp16x6 shapes it covers (A/B: NAIS_X6N=0 / 1
+// in the environment, read once per process; else the build's default)
+#ifndef NAIS_X6N_DEFAULT
+#define NAIS_X6N_DEFAULT 0
+#endif
+bool x6n_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NAIS_X6N");
+    return e && e[0] ? e[0] == '1' : NAIS_X6N_DEFAULT != 0;
+  }();
+  return on;
+}
+
 template <int DH, int HB, int VAR, int NPC = 2>
 int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                        const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                        const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
                        hipStream_t stream, const TableOut& tab = TableOut{}) {
+  if constexpr (NPC == 3 && !VarT<VAR>::DIST && (DH == 16 || DH == 32) && HB <= 2) {
+    if (x6n_enabled()) {
+      constexpr int D = 2 * DH, MB = 2 * HB;
+      constexpr bool REG = VarT<VAR>::REGION;
+      const size_t lds = CfgN<D, MB>::BYTES;
+      auto kern = catalog_score_x6n_kernel<D, MB, REG>;
+      static bool attr_set = false;
+      if (!attr_set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_set = true;
+      }
+      dim3 grid = tab.e ? table_grid(tab, nb, CfgN<D, MB>::CPB) : cat_grid(d.P, nb, CfgN<D, MB>::CPB);
+      hipLaunchKernelGGL(kern, grid, dim3(CfgN<D, MB>::THREADS), lds, stream, d, indptr, indices, users,
+                         region_of, scores, ld, nan_count, tab);
+      return check_launch("catalog_score_x6n_kernel");
+    }
+  }
   if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
