@@ -416,6 +416,17 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
     return out
 
 
+def table_kernel_name(precision, D, H):
+    """The catalog kernel nais_pair_table runs for this shape (nais_kernels.hip's dispatch)."""
+    if precision == "fp32":
+        return "catalog_score_kernel"
+    if precision.startswith("fp16x6") and D in (32, 64) and H <= 64 and os.environ.get("NAIS_X6N", "1") != "0":
+        return "catalog_score_x6n_kernel (16x16x32 f16 MFMA)"
+    if D > 64 or H > 64:
+        return "catalog_score_x3_kernel" if precision.startswith("fp16x6") else "catalog_score_x3b_kernel"
+    return "catalog_score_x3b_kernel"
+
+
 def self_launch(a):
     """--gpus N > 1 without a torchrun environment: start N fresh worker processes through
     torch.distributed.run (this process never touches the GPU) and return their exit code."""
@@ -643,9 +654,8 @@ def main():
                 "parallelism": f"users sharded (LPT) over {world} GPU(s), POI tables replicated",
             },
             "roofline": {
-                "kernel": ("catalog_score_kernel" if a.precision == "fp32" else
-                           "catalog_score_x3_kernel" if "pairsplit" in a.precision
-                           else "catalog_score_x3b_kernel") + " (nais_score_catalog)",
+                "kernel": ("catalog_score_x3_kernel" if "pairsplit" in a.precision
+                           else table_kernel_name(a.precision, D, H)) + " (nais_score_catalog)",
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": peak,
@@ -823,8 +833,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "launches_per_step": n_gl, "ms_per_step": g_ms, "cus": gcus,
         }
         table = {
-            "kernel": "catalog_score_x3b_kernel in table mode (nais_pair_table)" if precision != "fp32"
-                      else "catalog_score_kernel in table mode (nais_pair_table)",
+            "kernel": table_kernel_name(precision, D, H) + " in table mode (nais_pair_table)",
             "bound": "mfma", "achieved": t_ach, "peak": PEAKS[precision], "unit": "TFLOP/s",
             "frac": t_ach / PEAKS[precision] if t_ach else None,
             "frac_of_its_cus": t_ach / (PEAKS[precision] * table_cus / ncu) if t_ach else None,

@@ -2441,10 +2441,11 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
   }
 }
 
-// the 16x16x32 item-side kernel instead of x3b for the fp16x6 shapes it covers (A/B: NAIS_X6N=0 / 1
-// in the environment, read once per process; else the build's default)
+// the 16x16x32 item-side kernel instead of x3b for the fp16x6 shapes it covers (default since round
+// 4: standalone config-4 table block 2.179 -> 1.990 ms, the job 623 -> 601 ms, profiles/r4/x6n;
+// A/B: NAIS_X6N=0 / 1 in the environment, read once per process)
 #ifndef NAIS_X6N_DEFAULT
-#define NAIS_X6N_DEFAULT 0
+#define NAIS_X6N_DEFAULT 1
 #endif
 bool x6n_enabled() {
   static const bool on = [] {
