@@ -15,7 +15,8 @@ timeout -k 10 600 python bench.py > $out/bench.json 2> $out/bench.err || { tail 
 cut -c1-200 $out/bench.json
 timeout -k 10 300 python scripts/bench_table.py --blocks 8 --rounds 3 > $out/table_alone.txt 2>&1 || { tail -5 $out/table_alone.txt; exit 1; }
 tail -2 $out/table_alone.txt
-PMC_SETS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE|SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM" \
-  timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table x3b_kernel scripts/bench_table.py --blocks 8 --rounds 1 > $out/pmc.txt 2>&1
-echo "pmc rc=$?" >> $out/pmc.txt
-tail -30 $out/pmc.txt
+export PMC_SETS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE|SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM"
+timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table_x6n x6n_kernel scripts/bench_table.py --blocks 8 --rounds 1 > $out/pmc.txt 2>&1 || { tail -5 $out/pmc.txt; exit 1; }
+tail -20 $out/pmc.txt
+NAIS_X6N=0 timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table_x3b x3b_kernel scripts/bench_table.py --blocks 8 --rounds 1 > $out/pmc_x3b.txt 2>&1 || { tail -5 $out/pmc_x3b.txt; exit 1; }
+tail -20 $out/pmc_x3b.txt
