@@ -420,7 +420,7 @@ def table_kernel_name(precision, D, H):
     """The catalog kernel nais_pair_table runs for this shape (nais_kernels.hip's dispatch)."""
     if precision == "fp32":
         return "catalog_score_kernel"
-    if precision.startswith("fp16x6") and D in (32, 64) and H <= 64 and os.environ.get("NAIS_X6N", "1") != "0":
+    if precision.startswith("fp16x6") and D in (32, 64, 128) and H <= 128 and os.environ.get("NAIS_X6N", "1") != "0":
         return "catalog_score_x6n_kernel (16x16x32 f16 MFMA)"
     if D > 64 or H > 64:
         return "catalog_score_x3_kernel" if precision.startswith("fp16x6") else "catalog_score_x3b_kernel"

@@ -1430,35 +1430,42 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
   return c;
 }
 
-template <int D, int MB>   // D input dims (a multiple of 32), MB blocks of 16 hidden units
+// A "unit" is one item's A_j restricted to MB blocks of 16 hidden units; NHU units make the item,
+// whose logit partials are summed before the tail. The ring holds 2 groups of GU units: GU = 2
+// where a unit is <= 24 KiB, else 1 (a whole D = H = 128 item, 96 KiB, does not fit twice in the
+// 160 KiB LDS, hence units).
+template <int D, int MB, int NHU>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
-  static constexpr int NE = MB * KS * 64;              // uint4 entries per item and piece
-  static constexpr int IB = NE * 16 * 3;               // LDS bytes per item (three pieces)
-  static constexpr int G = 2;                          // items per ring group (even: two acc sets)
+  static constexpr int NE = MB * KS * 64;              // uint4 entries per unit and piece
+  static constexpr int IB = NE * 16 * 3;               // LDS bytes per unit (three pieces)
+  static constexpr int GU = IB <= 24576 ? 2 : 1;       // units per ring group
   static constexpr int JCB = 32;                       // chunk rows (the s tile's items)
   static constexpr int NW = 8, THREADS = NW * 64, CPB = NW * 32;
-  static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread
-  static constexpr int HP = MB * 16;                   // hidden units, padded
+  static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread and unit
+  static constexpr int HPU = MB * 16;                  // hidden units per unit
+  static constexpr int HP = HPU * NHU;                 // hidden units, padded
   static constexpr int EPI = 2 * HP;                   // [b1 | w2] by hidden unit
   static constexpr int SVP = JCB + 1;                  // s image pitch (floats): [cand][item]
-  static constexpr size_t BYTES = size_t(2) * G * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
+  static constexpr size_t BYTES = size_t(2) * GU * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
                                   size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4;
+  static_assert(BYTES <= 160 * 1024, "x6n: LDS");
 };
 
-template <int D, int MB, bool REGION>
+template <int D, int MB, int NHU, bool REGION>
 __global__ void __launch_bounds__(512, 1)
 catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                          const int64_t* __restrict__ region_of, float* __restrict__ scores,
                          int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
-  using C = CfgN<D, MB>;
-  constexpr int KS = C::KS, NE = C::NE, G = C::G, JCB = C::JCB, EPT = C::EPT, HP = C::HP;
-  constexpr int EPI = C::EPI, NW = C::NW, THREADS = C::THREADS, CPB = C::CPB, SVP = C::SVP;
+  using C = CfgN<D, MB, NHU>;
+  constexpr int KS = C::KS, NE = C::NE, GU = C::GU, JCB = C::JCB, EPT = C::EPT, HP = C::HP;
+  constexpr int HPU = C::HPU, EPI = C::EPI, NW = C::NW, THREADS = C::THREADS, CPB = C::CPB;
+  constexpr int SVP = C::SVP;
   constexpr int DH = D / 2;   // region variants: dims [DH, D) come from embed_region
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* ring = reinterpret_cast<uint4*>(smem);                    // [2 groups][G items][piece][NE]
-  float* Eimg = reinterpret_cast<float*>(ring + 2 * G * 3 * NE);   // [b1 | w2] by hidden unit
+  uint4* ring = reinterpret_cast<uint4*>(smem);                    // [2 groups][GU units][piece][NE]
+  float* Eimg = reinterpret_cast<float*>(ring + 2 * GU * 3 * NE);  // [b1 | w2] by hidden unit
   float* Escl = Eimg + EPI;                                        // per wave [S*b1 | w2/S]
   float* red = Escl + NW * EPI;
   float* hrows = red + 16;                                         // [JCB][D]
@@ -1482,20 +1489,22 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   const int64_t cout = cbase + 16 * (lane >> 5) + l16;
   const bool vout = cout < clim;
 
-  // ---- this thread's W1 values for its build entries (fp32, unscaled)
-  float wv[EPT][8];
+  // ---- this thread's W1 values for its build entries of every unit (fp32, unscaled)
+  float wv[NHU][EPT][8];
   float wmax = 0.f;
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * THREADS;
-    const int ln = e & 63, s = (e >> 6) % KS, m = (e >> 6) / KS;
-    const int i = 16 * m + (ln & 15), k0 = 32 * s + 8 * (ln >> 4);
+  for (int h = 0; h < NHU; ++h)
 #pragma unroll
-    for (int x = 0; x < 8; ++x) {
-      wv[q][x] = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
-      wmax = fmaxf(wmax, fabsf(wv[q][x]));
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * THREADS;
+      const int ln = e & 63, s = (e >> 6) % KS, m = (e >> 6) / KS;
+      const int i = HPU * h + 16 * m + (ln & 15), k0 = 32 * s + 8 * (ln >> 4);
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        wv[h][q][x] = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
+        wmax = fmaxf(wmax, fabsf(wv[h][q][x]));
+      }
     }
-  }
   for (int f = tid; f < EPI; f += THREADS) {
     const int i = f % HP;
     Eimg[f] = (i < p.H) ? (f < HP ? p.b1[i] : p.w2[i]) : 0.f;
@@ -1506,7 +1515,6 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   half8 tb[2][KS][3];
   float St;
   {
-    float tv[2][KS][8];
     float tmax = 0.f;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
@@ -1519,24 +1527,28 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
                                                 : p.et + cc * p.item_dim + k0;
         const float4 v0 = reinterpret_cast<const float4*>(src)[0];
         const float4 v1 = reinterpret_cast<const float4*>(src)[1];
-        tv[nb][s][0] = v0.x; tv[nb][s][1] = v0.y; tv[nb][s][2] = v0.z; tv[nb][s][3] = v0.w;
-        tv[nb][s][4] = v1.x; tv[nb][s][5] = v1.y; tv[nb][s][6] = v1.z; tv[nb][s][7] = v1.w;
-#pragma unroll
-        for (int x = 0; x < 8; ++x) tmax = fmaxf(tmax, fabsf(tv[nb][s][x]));
+        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
+                                 fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)))));
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
     St = pow2_scale(tmax);
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+    for (int nb = 0; nb < 2; ++nb) {   // second read of the rows (L1 / L2 hits): fewer live VGPRs
+      const int64_t c = cbase + 16 * nb + l16;
+      const int64_t cc = c < clim ? c : p.P - 1;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = tv[nb][s][e] * St;
+        const int k0 = 32 * s + 8 * grp;
+        const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
+                                                : p.et + cc * p.item_dim + k0;
+        const float4 v0 = reinterpret_cast<const float4*>(src)[0];
+        const float4 v1 = reinterpret_cast<const float4*>(src)[1];
+        float x[8] = {v0.x * St, v0.y * St, v0.z * St, v0.w * St, v1.x * St, v1.y * St, v1.z * St, v1.w * St};
         split_pieces<3>(x, tb[nb][s]);
       }
+    }
   }
 
   float S = 0.f, N = 0.f;
@@ -1546,10 +1558,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* sv_mine = svt + wave * 32 * SVP;
   float SAcur = 1.f;
   int64_t j0 = 0;
+  float pa0 = 0.f, pa1 = 0.f;                 // logit partials of the item's earlier units
 
-  auto build = [&](int jj, int grp_, int it) {   // chunk item jj's fragments into ring slot (grp_, it)
+  // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it)
+  auto build = [&](int u, int grp_, int it) {
+    const int jj = u / NHU, h = u % NHU;
     const float* hr = hrows + jj * D;
-    uint4* dst = ring + ((grp_ * G + it) * 3) * NE;
+    uint4* dst = ring + ((grp_ * GU + it) * 3) * NE;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * THREADS;
@@ -1558,9 +1573,18 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         const int k0 = 32 * s + 8 * (ln >> 4);
         const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
         const float4 h1 = *reinterpret_cast<const float4*>(hr + k0 + 4);
+        float w[8];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) w[x] = wv[0][q][x];
+#pragma unroll
+        for (int hh = 1; hh < NHU; ++hh)   // h is block-uniform: selects, no indexed registers
+          if (h == hh) {
+#pragma unroll
+            for (int x = 0; x < 8; ++x) w[x] = wv[hh][q][x];
+          }
         float a[8];
-        a[0] = wv[q][0] * h0.x; a[1] = wv[q][1] * h0.y; a[2] = wv[q][2] * h0.z; a[3] = wv[q][3] * h0.w;
-        a[4] = wv[q][4] * h1.x; a[5] = wv[q][5] * h1.y; a[6] = wv[q][6] * h1.z; a[7] = wv[q][7] * h1.w;
+        a[0] = w[0] * h0.x; a[1] = w[1] * h0.y; a[2] = w[2] * h0.z; a[3] = w[3] * h0.w;
+        a[4] = w[4] * h1.x; a[5] = w[5] * h1.y; a[6] = w[6] * h1.z; a[7] = w[7] * h1.w;
         half8 pc[3];
         split_pieces<3>(a, pc);
 #pragma unroll
@@ -1594,19 +1618,22 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
   };
 
-  // item `cur`'s MFMAs (ring slot src) into accN, with the epilogue of item `prev` (accP) cut into
-  // slices between them
+  // unit `cur`'s MFMAs (ring slot src) into accN, with the epilogue of unit `prev` (accP) cut into
+  // slices between them; after the epilogue of an item's last unit, its tail
   auto step = [&](auto do_mma, const uint4* src, floatx4 (&accN)[MB][2], const floatx4 (&accP)[MB][2],
-                  int prev, bool live) {
+                  int cur, int prev, bool live) {
     constexpr bool MMA = decltype(do_mma)::value;
-    constexpr int NU = KS * MB;                 // (s, m) units of 12 MFMAs
+    constexpr int NU = KS * MB;                 // (s, m) work steps of 12 MFMAs
     constexpr int NV = 2 * MB;                  // epilogue slices: (nb, m), 4 values each
     constexpr int VPU = (NV + NU - 1) / NU;
+    const int hc = cur % NHU, hp = prev >= 0 ? prev % NHU : 0;
+    const float* ebc = eb + HPU * hc;
+    const float* ewp = ew + HPU * hp;
     float ap0 = 0.f, ap1 = 0.f;
     if (MMA) {
 #pragma unroll
       for (int m = 0; m < MB; ++m) {
-        const float4 b4 = *reinterpret_cast<const float4*>(eb + 16 * m + 4 * grp);
+        const float4 b4 = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) {
           accN[m][nb][0] = b4.x; accN[m][nb][1] = b4.y; accN[m][nb][2] = b4.z; accN[m][nb][3] = b4.w;
@@ -1629,7 +1656,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
       for (int v = u * VPU; v < (u + 1) * VPU && v < NV; ++v) {
         const int nb = v / MB, mm = v % MB;
-        const float4 w4 = *reinterpret_cast<const float4*>(ew + 16 * mm + 4 * grp);
+        const float4 w4 = *reinterpret_cast<const float4*>(ewp + 16 * mm + 4 * grp);
         float t = nb ? ap1 : ap0;
         t = __builtin_fmaf(w4.x, relu_bits(accP[mm][nb][0]), t);
         t = __builtin_fmaf(w4.y, relu_bits(accP[mm][nb][1]), t);
@@ -1638,7 +1665,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (nb) ap1 = t; else ap0 = t;
       }
     }
-    tail(prev >= 0 ? prev : 0, ap0, ap1, live);
+    if constexpr (NHU == 1) {
+      tail(prev >= 0 ? prev : 0, ap0, ap1, live);
+    } else {                     // an item's units add their partials; its last one, the tail
+      pa0 = hp == 0 ? ap0 : pa0 + ap0;
+      pa1 = hp == 0 ? ap1 : pa1 + ap1;
+      if (hp == NHU - 1) tail(prev / NHU, pa0, pa1, live);
+    }
   };
 
   floatx4 acc2[2][MB][2];
@@ -1662,9 +1695,11 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const float SA = pow2_scale(Wmax * Hm);
     const float rs = SA / SAcur;                   // exact power-of-two ratio
 #pragma unroll
-    for (int q = 0; q < EPT; ++q)
+    for (int h = 0; h < NHU; ++h)
 #pragma unroll
-      for (int x = 0; x < 8; ++x) wv[q][x] *= rs;
+      for (int q = 0; q < EPT; ++q)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) wv[h][q][x] *= rs;
     SAcur = SA;
     const float Sacc = SA * St, invS = 1.f / Sacc;
     for (int f = lane; f < EPI; f += 64) Escl[wave * EPI + f] = Eimg[f] * (f < HP ? Sacc : invS);
@@ -1705,36 +1740,49 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
           for (int r = 0; r < 4; ++r)
             sv_mine[(16 * nb + l16) * SVP + 16 * mi + 4 * grp + r] = sacc[mi][nb][r] * invShSt;
     }
-    const int ngroups = (jn + G - 1) / G;
+    const int nunits = jn * NHU;
+    const int ngroups = (nunits + GU - 1) / GU;
 #pragma unroll
-    for (int it = 0; it < G; ++it)
-      if (it < jn) build(it, 0, it);
+    for (int it = 0; it < GU; ++it)
+      if (it < nunits) build(it, 0, it);
     __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
     int prev = -1;
-    for (int g = 0; g < ngroups; ++g) {
+    // one group: build the next group, then this group's units; units alternate the two
+    // accumulator sets by their parity, which is compile-time here: GU = 2 (it) or GU = 1 (the
+    // group's parity, the loop below takes groups in pairs)
+    auto group = [&](int g, auto gpar) {
+      constexpr int GP = decltype(gpar)::value;
       if (g + 1 < ngroups) {
 #pragma unroll
-        for (int it = 0; it < G; ++it) {
-          const int jj = (g + 1) * G + it;
-          if (jj < jn) build(jj, (g + 1) & 1, it);
+        for (int it = 0; it < GU; ++it) {
+          const int u = (g + 1) * GU + it;
+          if (u < nunits) build(u, (g + 1) & 1, it);
         }
       }
 #pragma unroll
-      for (int it = 0; it < G; ++it) {
-        const int jj = g * G + it;
-        if (jj < jn) {
-          const uint4* src = ring + (((g & 1) * G + it) * 3) * NE;
-          step(std::true_type{}, src, acc2[it & 1], acc2[(it + 1) & 1], prev, prev >= 0);
-          prev = jj;
+      for (int it = 0; it < GU; ++it) {
+        const int u = g * GU + it;
+        if (u < nunits) {
+          const uint4* src = ring + ((GP * GU + it) * 3) * NE;
+          constexpr int P0 = (GU == 2) ? 0 : GP;   // parity of the group's first unit
+          if ((P0 + it) & 1)
+            step(std::true_type{}, src, acc2[1], acc2[0], u, prev, prev >= 0);
+          else
+            step(std::true_type{}, src, acc2[0], acc2[1], u, prev, prev >= 0);
+          prev = u;
         }
       }
       __syncthreads();
+    };
+    for (int g = 0; g < ngroups; g += 2) {
+      group(g, std::integral_constant<int, 0>{});
+      if (g + 1 < ngroups) group(g + 1, std::integral_constant<int, 1>{});
     }
-    if (prev >= 0) {   // drain: the epilogue of the chunk's last item, no MFMAs
+    if (prev >= 0) {   // drain: the epilogue of the chunk's last unit, no MFMAs
       if (prev & 1)
-        step(std::false_type{}, ring, acc2[0], acc2[1], prev, true);
+        step(std::false_type{}, ring, acc2[0], acc2[1], prev, prev, true);
       else
-        step(std::false_type{}, ring, acc2[1], acc2[0], prev, true);
+        step(std::false_type{}, ring, acc2[1], acc2[0], prev, prev, true);
     }
   }
   if (tab.e) return;
@@ -2460,20 +2508,25 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                        const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                        const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
                        hipStream_t stream, const TableOut& tab = TableOut{}) {
-  if constexpr (NPC == 3 && !VarT<VAR>::DIST && (DH == 16 || DH == 32) && HB <= 2) {
+  if constexpr (NPC == 3 && !VarT<VAR>::DIST && (DH == 16 || DH == 32 || DH == 64)) {
     if (x6n_enabled()) {
-      constexpr int D = 2 * DH, MB = 2 * HB;
+      // D <= 64: one unit up to 64 hidden units, two at H = 128; D = 128: units of 32 hidden
+      // units (MB = 4 would need more than the 256 VGPRs of two waves per SIMD)
+      constexpr int D = 2 * DH;
+      constexpr int MB = D == 128 ? 2 : (HB <= 2 ? 2 * HB : 4);
+      constexpr int NHU = D == 128 ? HB : (HB <= 2 ? 1 : 2);
       constexpr bool REG = VarT<VAR>::REGION;
-      const size_t lds = CfgN<D, MB>::BYTES;
-      auto kern = catalog_score_x6n_kernel<D, MB, REG>;
+      using CN = CfgN<D, MB, NHU>;
+      const size_t lds = CN::BYTES;
+      auto kern = catalog_score_x6n_kernel<D, MB, NHU, REG>;
       static bool attr_set = false;
       if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr_set = true;
       }
-      dim3 grid = tab.e ? table_grid(tab, nb, CfgN<D, MB>::CPB) : cat_grid(d.P, nb, CfgN<D, MB>::CPB);
-      hipLaunchKernelGGL(kern, grid, dim3(CfgN<D, MB>::THREADS), lds, stream, d, indptr, indices, users,
+      dim3 grid = tab.e ? table_grid(tab, nb, CN::CPB) : cat_grid(d.P, nb, CN::CPB);
+      hipLaunchKernelGGL(kern, grid, dim3(CN::THREADS), lds, stream, d, indptr, indices, users,
                          region_of, scores, ld, nan_count, tab);
       return check_launch("catalog_score_x6n_kernel");
     }
