@@ -1434,6 +1434,11 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 // whose logit partials are summed before the tail. The ring holds 2 groups of GU units: GU = 2
 // where a unit is <= 24 KiB, else 1 (a whole D = H = 128 item, 96 KiB, does not fit twice in the
 // 160 KiB LDS, hence units).
+// ablations for timing only (results are garbage): 1 no epilogue, 2 no build, 4 no A-fragment LDS
+// reads, 8 no tail, 16 no group barriers
+#ifndef NAIS_X6N_ABL
+#define NAIS_X6N_ABL 0
+#endif
 template <int D, int MB, int NHU>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
@@ -1560,7 +1565,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   int64_t j0 = 0;
   float pa0 = 0.f, pa1 = 0.f;                 // logit partials of the item's earlier units
 
-  // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it)
+  // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
+  // of the block size (the D = 64 / 128 shapes) it has no branch, so the scheduler can spread it
+  // between the MFMAs of the step it is called from.
   auto build = [&](int u, int grp_, int it) {
     const int jj = u / NHU, h = u % NHU;
     const float* hr = hrows + jj * D;
@@ -1568,7 +1575,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * THREADS;
-      if (e < NE) {
+      if (NE % THREADS == 0 || e < NE) {
         const int ln = e & 63, s = (e >> 6) % KS;
         const int k0 = 32 * s + 8 * (ln >> 4);
         const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
@@ -1578,10 +1585,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         for (int x = 0; x < 8; ++x) w[x] = wv[0][q][x];
 #pragma unroll
         for (int hh = 1; hh < NHU; ++hh)   // h is block-uniform: selects, no indexed registers
-          if (h == hh) {
 #pragma unroll
-            for (int x = 0; x < 8; ++x) w[x] = wv[hh][q][x];
-          }
+          for (int x = 0; x < 8; ++x) w[x] = h == hh ? wv[hh][q][x] : w[x];
         float a[8];
         a[0] = w[0] * h0.x; a[1] = w[1] * h0.y; a[2] = w[2] * h0.z; a[3] = w[3] * h0.w;
         a[4] = w[4] * h1.x; a[5] = w[5] * h1.y; a[6] = w[6] * h1.z; a[7] = w[7] * h1.w;
@@ -1594,7 +1599,10 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   };
 
   // the pair (chunk item pj, this lane's output candidate): the logit partials of the two candidate
-  // blocks summed over the lane groups, then e and e * s
+  // blocks summed over the lane groups, then e and e * s. No branches: the running sums take
+  // selects, and the table rows are written by buffer stores whose offset is out of range (the
+  // store dropped) for the lanes that do not write -- so the tail stays in the step's basic block.
+  const uint32_t tab_bytes = tab.e ? (uint32_t)(tab.cols * 4) : 0u;
   auto tail = [&](int pj, float p0, float p1, bool live) {
     const auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
     const float q = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);   // groups {g, g + 2}
@@ -1603,25 +1611,22 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const float sv = sv_mine[(16 * (lane >> 5) + l16) * SVP + pj];
     const bool keep = hid[pj] != (int32_t)cout;
     const float e = expf(a) * (keep ? 1.f : 0.f);
-    if (live) {
-      if (tab.e) {
-        if (vout) {
-          const int64_t o = (hbeg + j0 + pj) * tab.ld + (cout - tab.col0);
-          if (grp & 1) tab.es[o] = e * sv;
-          else tab.e[o] = e;
-        }
-      } else {
-        in_hist |= !keep;
-        S += e;
-        N += e * sv;
-      }
-    }
+    in_hist |= live && !keep;
+    S += live ? e : 0.f;
+    N += live ? e * sv : 0.f;
+    const int64_t row = (hbeg + j0 + pj) * tab.ld;
+    const int off = (live && vout) ? (int)(cout - tab.col0) * 4 : (int)0x80000000;
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(tab.e + row, (short)0, tab_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tab.es + row, (short)0, tab_bytes, 0x00020000);
+    const bool odd = grp & 1;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), re, odd ? (int)0x80000000 : off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e * sv), rs, odd ? off : (int)0x80000000, 0, 0);
   };
 
   // unit `cur`'s MFMAs (ring slot src) into accN, with the epilogue of unit `prev` (accP) cut into
   // slices between them; after the epilogue of an item's last unit, its tail
   auto step = [&](auto do_mma, const uint4* src, floatx4 (&accN)[MB][2], const floatx4 (&accP)[MB][2],
-                  int cur, int prev, bool live) {
+                  int cur, int prev, bool live, int bu, int bgrp, int bit) {
     constexpr bool MMA = decltype(do_mma)::value;
     constexpr int NU = KS * MB;                 // (s, m) work steps of 12 MFMAs
     constexpr int NV = 2 * MB;                  // epilogue slices: (nb, m), 4 values each
@@ -1647,14 +1652,19 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         half8 a_[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
-          a_[q] = *reinterpret_cast<const half8*>(&u4);
+          if (NAIS_X6N_ABL & 4) {
+            a_[q] = tb[1][s][q];
+          } else {
+            const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
+            a_[q] = *reinterpret_cast<const half8*>(&u4);
+          }
         }
         accN[m][0] = mfma16n_pieces(a_, tb[0][s], accN[m][0]);
         accN[m][1] = mfma16n_pieces(a_, tb[1][s], accN[m][1]);
+        if (!(NAIS_X6N_ABL & 2) && u == NU - 1) build(bu, bgrp, bit);   // a unit of the next group, between the MFMAs
       }
 #pragma unroll
-      for (int v = u * VPU; v < (u + 1) * VPU && v < NV; ++v) {
+      for (int v = u * VPU; !(NAIS_X6N_ABL & 1) && v < (u + 1) * VPU && v < NV; ++v) {
         const int nb = v / MB, mm = v % MB;
         const float4 w4 = *reinterpret_cast<const float4*>(ewp + 16 * mm + 4 * grp);
         float t = nb ? ap1 : ap0;
@@ -1665,7 +1675,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (nb) ap1 = t; else ap0 = t;
       }
     }
-    if constexpr (NHU == 1) {
+    if (NAIS_X6N_ABL & 1) {
+      ap0 = accP[0][0][0];
+      ap1 = accP[MB - 1][1][3];
+    }
+    if (NAIS_X6N_ABL & 8) {
+      S += ap0 + ap1;
+    } else if constexpr (NHU == 1) {
       tail(prev >= 0 ? prev : 0, ap0, ap1, live);
     } else {                     // an item's units add their partials; its last one, the tail
       pa0 = hp == 0 ? ap0 : pa0 + ap0;
@@ -1746,43 +1762,36 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     for (int it = 0; it < GU; ++it)
       if (it < nunits) build(it, 0, it);
     __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
-    int prev = -1;
-    // one group: build the next group, then this group's units; units alternate the two
+    // one group: its units' steps, each building a unit of the next group (past the chunk's end a
+    // clamped copy nobody reads) and finishing the previous unit; units alternate the two
     // accumulator sets by their parity, which is compile-time here: GU = 2 (it) or GU = 1 (the
-    // group's parity, the loop below takes groups in pairs)
+    // group's parity, the loop below takes groups in pairs). With GU = 2 and an odd unit count the
+    // last step runs on a stale slot: only its epilogue of the unit before it is used.
     auto group = [&](int g, auto gpar) {
       constexpr int GP = decltype(gpar)::value;
-      if (g + 1 < ngroups) {
-#pragma unroll
-        for (int it = 0; it < GU; ++it) {
-          const int u = (g + 1) * GU + it;
-          if (u < nunits) build(u, (g + 1) & 1, it);
-        }
-      }
 #pragma unroll
       for (int it = 0; it < GU; ++it) {
         const int u = g * GU + it;
-        if (u < nunits) {
-          const uint4* src = ring + ((GP * GU + it) * 3) * NE;
-          constexpr int P0 = (GU == 2) ? 0 : GP;   // parity of the group's first unit
-          if ((P0 + it) & 1)
-            step(std::true_type{}, src, acc2[1], acc2[0], u, prev, prev >= 0);
-          else
-            step(std::true_type{}, src, acc2[0], acc2[1], u, prev, prev >= 0);
-          prev = u;
-        }
+        const int bu = std::min(u + GU, nunits - 1);
+        const uint4* src = ring + ((GP * GU + it) * 3) * NE;
+        constexpr int P0 = (GU == 2) ? 0 : GP;   // parity of the group's first unit
+        if ((P0 + it) & 1)
+          step(std::true_type{}, src, acc2[1], acc2[0], u, u - 1, u > 0, bu, GP ^ 1, it);
+        else
+          step(std::true_type{}, src, acc2[0], acc2[1], u, u - 1, u > 0, bu, GP ^ 1, it);
       }
-      __syncthreads();
+      if (!(NAIS_X6N_ABL & 16)) __syncthreads();
     };
     for (int g = 0; g < ngroups; g += 2) {
       group(g, std::integral_constant<int, 0>{});
       if (g + 1 < ngroups) group(g + 1, std::integral_constant<int, 1>{});
     }
-    if (prev >= 0) {   // drain: the epilogue of the chunk's last unit, no MFMAs
-      if (prev & 1)
-        step(std::false_type{}, ring, acc2[0], acc2[1], prev, prev, true);
+    const int last = ngroups * GU - 1;   // the last step's unit
+    if (last == nunits - 1) {            // drain: the epilogue of the chunk's last unit, no MFMAs
+      if (last & 1)
+        step(std::false_type{}, ring, acc2[0], acc2[1], last, last, true, 0, 0, 0);
       else
-        step(std::false_type{}, ring, acc2[1], acc2[0], prev, prev, true);
+        step(std::false_type{}, ring, acc2[1], acc2[0], last, last, true, 0, 0, 0);
     }
   }
   if (tab.e) return;

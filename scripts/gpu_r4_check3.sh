@@ -20,3 +20,7 @@ timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table_x6n x6n_kernel scripts/bench_ta
 tail -20 $out/pmc.txt
 NAIS_X6N=0 timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table_x3b x3b_kernel scripts/bench_table.py --blocks 8 --rounds 1 > $out/pmc_x3b.txt 2>&1 || { tail -5 $out/pmc_x3b.txt; exit 1; }
 tail -20 $out/pmc_x3b.txt
+timeout -k 10 300 python scripts/bench_table.py --dim 128 --hidden 128 --blocks 4 --rounds 3 > $out/table128_alone.txt 2>&1 || { tail -5 $out/table128_alone.txt; exit 1; }
+tail -2 $out/table128_alone.txt
+timeout -k 10 600 scripts/gpu_pmc_cmd.sh r4table_x6n128 x6n_kernel scripts/bench_table.py --dim 128 --hidden 128 --blocks 4 --rounds 1 > $out/pmc128.txt 2>&1 || { tail -5 $out/pmc128.txt; exit 1; }
+tail -20 $out/pmc128.txt
