@@ -1439,6 +1439,19 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 #ifndef NAIS_X6N_ABL
 #define NAIS_X6N_ABL 0
 #endif
+#ifndef NAIS_X6N_BPOS
+#define NAIS_X6N_BPOS -1
+#endif
+#ifndef NAIS_X6N_PREF
+#define NAIS_X6N_PREF 1
+#endif
+// compile-time hidden slices of one x6n step: the unit it multiplies, the unit it finishes and the
+// unit it builds
+template <int C, int P, int B>
+struct X6Slices {
+  static constexpr int cur = C, prev = P, built = B;
+};
+
 template <int D, int MB, int NHU>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
@@ -1455,6 +1468,7 @@ struct CfgN {
   static constexpr size_t BYTES = size_t(2) * GU * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
                                   size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4;
   static_assert(BYTES <= 160 * 1024, "x6n: LDS");
+  static_assert((2 * GU) % NHU == 0, "x6n: a group pair spans whole items");
 };
 
 template <int D, int MB, int NHU, bool REGION>
@@ -1568,9 +1582,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
   // of the block size (the D = 64 / 128 shapes) it has no branch, so the scheduler can spread it
   // between the MFMAs of the step it is called from.
-  auto build = [&](int u, int grp_, int it) {
-    const int jj = u / NHU, h = u % NHU;
-    const float* hr = hrows + jj * D;
+  auto build = [&](int u, auto hsc, int grp_, int it) {
+    constexpr int HS = decltype(hsc)::value;   // the unit's hidden slice (u % NHU where it matters)
+    const float* hr = hrows + (u / NHU) * D;
     uint4* dst = ring + ((grp_ * GU + it) * 3) * NE;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
@@ -1580,13 +1594,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         const int k0 = 32 * s + 8 * (ln >> 4);
         const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
         const float4 h1 = *reinterpret_cast<const float4*>(hr + k0 + 4);
-        float w[8];
-#pragma unroll
-        for (int x = 0; x < 8; ++x) w[x] = wv[0][q][x];
-#pragma unroll
-        for (int hh = 1; hh < NHU; ++hh)   // h is block-uniform: selects, no indexed registers
-#pragma unroll
-          for (int x = 0; x < 8; ++x) w[x] = h == hh ? wv[hh][q][x] : w[x];
+        const float* w = wv[HS][q];
         float a[8];
         a[0] = w[0] * h0.x; a[1] = w[1] * h0.y; a[2] = w[2] * h0.z; a[3] = w[3] * h0.w;
         a[4] = w[4] * h1.x; a[5] = w[5] * h1.y; a[6] = w[6] * h1.z; a[7] = w[7] * h1.w;
@@ -1623,74 +1631,100 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e * sv), rs, odd ? off : (int)0x80000000, 0, 0);
   };
 
-  // unit `cur`'s MFMAs (ring slot src) into accN, with the epilogue of unit `prev` (accP) cut into
-  // slices between them; after the epilogue of an item's last unit, its tail
-  auto step = [&](auto do_mma, const uint4* src, floatx4 (&accN)[MB][2], const floatx4 (&accP)[MB][2],
-                  int cur, int prev, bool live, int bu, int bgrp, int bit) {
+  // One unit per step, in block-major order: block m (16 hidden units) takes its KS groups of 12
+  // MFMAs (KS = D / 32) into acc[m & 1], and the epilogue of the block before it (w2 . ReLU, 8
+  // values per lane) runs one group later, between block m's MFMAs -- so only two blocks'
+  // accumulators are live (16 VGPRs instead of a whole second unit's). Block 0's epilogue slot
+  // finishes the previous unit (its last block, then its tail); the unit's own blocks 0 .. MB - 2
+  // accumulate into apc. The hidden slices of cur / prev / the unit built (bu) are compile-time
+  // (X6Slices): the slice's W1 registers, b1 / w2 offsets and the item's tail are fixed per call
+  // site -- no selects, no branches. A fragments are read one group ahead.
+  static_assert(MB % 2 == 0, "x6n: block parity is compile-time");
+  floatx4 acc[2][2];
+  float apc0 = 0.f, apc1 = 0.f;
+  auto epi = [&](const float* ewb, const floatx4 (&a)[2], float& t0, float& t1) {
+    const float4 w4 = *reinterpret_cast<const float4*>(ewb + 4 * grp);
+    t0 = __builtin_fmaf(w4.x, relu_bits(a[0][0]), t0);
+    t0 = __builtin_fmaf(w4.y, relu_bits(a[0][1]), t0);
+    t0 = __builtin_fmaf(w4.z, relu_bits(a[0][2]), t0);
+    t0 = __builtin_fmaf(w4.w, relu_bits(a[0][3]), t0);
+    t1 = __builtin_fmaf(w4.x, relu_bits(a[1][0]), t1);
+    t1 = __builtin_fmaf(w4.y, relu_bits(a[1][1]), t1);
+    t1 = __builtin_fmaf(w4.z, relu_bits(a[1][2]), t1);
+    t1 = __builtin_fmaf(w4.w, relu_bits(a[1][3]), t1);
+  };
+  auto step = [&](auto do_mma, auto sl, const uint4* src, int cur, int prev, bool live, int bu, int bgrp,
+                  int bit) {
     constexpr bool MMA = decltype(do_mma)::value;
-    constexpr int NU = KS * MB;                 // (s, m) work steps of 12 MFMAs
-    constexpr int NV = 2 * MB;                  // epilogue slices: (nb, m), 4 values each
-    constexpr int VPU = (NV + NU - 1) / NU;
-    const int hc = cur % NHU, hp = prev >= 0 ? prev % NHU : 0;
-    const float* ebc = eb + HPU * hc;
-    const float* ewp = ew + HPU * hp;
-    float ap0 = 0.f, ap1 = 0.f;
-    if (MMA) {
+    constexpr int HC = decltype(sl)::cur, HPV = decltype(sl)::prev, HB = decltype(sl)::built;
+    constexpr int NG = KS * MB;                 // (m, s) groups of 12 MFMAs
+    constexpr int EG = KS > 1 ? 1 : 0;          // a block's epilogue slot: its successor's group EG
+    const float* ebc = eb + HPU * HC;
+    const float* ewc = ew + HPU * HC;
+    const float* ewp = ew + HPU * HPV + 16 * (MB - 1);
+    (void)cur;
+    auto aload = [&](int g, half8 (&a)[3]) {
+      const int m = g / KS, s = g % KS;
 #pragma unroll
-      for (int m = 0; m < MB; ++m) {
-        const float4 b4 = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-          accN[m][nb][0] = b4.x; accN[m][nb][1] = b4.y; accN[m][nb][2] = b4.z; accN[m][nb][3] = b4.w;
+      for (int q = 0; q < 3; ++q) {
+        if (NAIS_X6N_ABL & 4) {
+          a[q] = tb[1][s][q];
+        } else {
+          const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
+          a[q] = *reinterpret_cast<const half8*>(&u4);
         }
       }
-    }
+    };
+    half8 a_nx[3];
+    if (MMA) aload(0, a_nx);
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int s = u / MB, m = u % MB;
+    for (int g = 0; g < NG; ++g) {
+      const int m = g / KS, s = g % KS;
       if (MMA) {
-        half8 a_[3];
+        if (s == 0) {   // the block's accumulators start at S*b1 (the MFMA's C operand)
+          const float4 b4 = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          if (NAIS_X6N_ABL & 4) {
-            a_[q] = tb[1][s][q];
-          } else {
-            const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
-            a_[q] = *reinterpret_cast<const half8*>(&u4);
+          for (int nb = 0; nb < 2; ++nb) {
+            acc[m & 1][nb][0] = b4.x; acc[m & 1][nb][1] = b4.y;
+            acc[m & 1][nb][2] = b4.z; acc[m & 1][nb][3] = b4.w;
           }
         }
-        accN[m][0] = mfma16n_pieces(a_, tb[0][s], accN[m][0]);
-        accN[m][1] = mfma16n_pieces(a_, tb[1][s], accN[m][1]);
-        if (!(NAIS_X6N_ABL & 2) && u == NU - 1) build(bu, bgrp, bit);   // a unit of the next group, between the MFMAs
-      }
+        half8 a_[3];
 #pragma unroll
-      for (int v = u * VPU; !(NAIS_X6N_ABL & 1) && v < (u + 1) * VPU && v < NV; ++v) {
-        const int nb = v / MB, mm = v % MB;
-        const float4 w4 = *reinterpret_cast<const float4*>(ewp + 16 * mm + 4 * grp);
-        float t = nb ? ap1 : ap0;
-        t = __builtin_fmaf(w4.x, relu_bits(accP[mm][nb][0]), t);
-        t = __builtin_fmaf(w4.y, relu_bits(accP[mm][nb][1]), t);
-        t = __builtin_fmaf(w4.z, relu_bits(accP[mm][nb][2]), t);
-        t = __builtin_fmaf(w4.w, relu_bits(accP[mm][nb][3]), t);
-        if (nb) ap1 = t; else ap0 = t;
+        for (int q = 0; q < 3; ++q) a_[q] = a_nx[q];
+        if (g + 1 < NG) aload(g + 1, a_nx);
+        acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
+        acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
+        if (!(NAIS_X6N_ABL & 2) && g == (NAIS_X6N_BPOS < 0 ? NG - 1 : NAIS_X6N_BPOS * NG / 4))
+          build(bu, std::integral_constant<int, HB>{}, bgrp, bit);   // a unit of the next group
+      }
+      if (s != EG || NAIS_X6N_ABL & 1) continue;
+      if (m == 0) {   // the previous unit's last block, then that unit is complete
+        float ap0 = apc0, ap1 = apc1;
+        epi(ewp, acc[(MB - 1) & 1], ap0, ap1);
+        apc0 = 0.f;
+        apc1 = 0.f;
+        if (NAIS_X6N_ABL & 8) {
+          S += ap0 + ap1;
+        } else if constexpr (NHU == 1) {
+          tail(prev >= 0 ? prev : 0, ap0, ap1, live);
+        } else {                 // an item's units add their partials; its last one, the tail
+          pa0 = HPV == 0 ? ap0 : pa0 + ap0;
+          pa1 = HPV == 0 ? ap1 : pa1 + ap1;
+          if constexpr (HPV == NHU - 1) tail(prev < 0 ? 0 : prev / NHU, pa0, pa1, live);
+        }
+      } else if (MMA) {
+        epi(ewc + 16 * (m - 1), acc[(m - 1) & 1], apc0, apc1);
       }
     }
-    if (NAIS_X6N_ABL & 1) {
-      ap0 = accP[0][0][0];
-      ap1 = accP[MB - 1][1][3];
-    }
-    if (NAIS_X6N_ABL & 8) {
-      S += ap0 + ap1;
-    } else if constexpr (NHU == 1) {
-      tail(prev >= 0 ? prev : 0, ap0, ap1, live);
-    } else {                     // an item's units add their partials; its last one, the tail
-      pa0 = hp == 0 ? ap0 : pa0 + ap0;
-      pa1 = hp == 0 ? ap1 : pa1 + ap1;
-      if (hp == NHU - 1) tail(prev / NHU, pa0, pa1, live);
+    if (NAIS_X6N_ABL & 1) {   // keep every accumulator alive without VALU work
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) asm volatile("" ::"v"(acc[k][nb]));
     }
   };
 
-  floatx4 acc2[2][MB][2];
   for (j0 = 0; j0 < hlen; j0 += JCB) {
     const int jn = (int)std::min<int64_t>(JCB, hlen - j0);
     __syncthreads();   // the previous chunk's ring, hrows and hid readers are done
@@ -1758,28 +1792,26 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
     const int nunits = jn * NHU;
     const int ngroups = (nunits + GU - 1) / GU;
-#pragma unroll
-    for (int it = 0; it < GU; ++it)
-      if (it < nunits) build(it, 0, it);
+    build(0, std::integral_constant<int, 0>{}, 0, 0);
+    if (GU == 2 && nunits > 1) build(1, std::integral_constant<int, 1 % NHU>{}, 0, 1);
     __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
     // one group: its units' steps, each building a unit of the next group (past the chunk's end a
-    // clamped copy nobody reads) and finishing the previous unit; units alternate the two
-    // accumulator sets by their parity, which is compile-time here: GU = 2 (it) or GU = 1 (the
-    // group's parity, the loop below takes groups in pairs). With GU = 2 and an odd unit count the
-    // last step runs on a stale slot: only its epilogue of the unit before it is used.
+    // clamped copy nobody reads) and finishing the previous unit; groups go in pairs, so every
+    // step's hidden slices are compile-time. With GU = 2 and an odd unit count the last step runs
+    // on a stale slot: only its finish of the unit before it is used.
     auto group = [&](int g, auto gpar) {
       constexpr int GP = decltype(gpar)::value;
-#pragma unroll
-      for (int it = 0; it < GU; ++it) {
+      auto one = [&](auto itc) {
+        constexpr int it = decltype(itc)::value;
+        constexpr int HC = (GP * GU + it) % NHU;   // u % NHU: a group pair spans 2 GU units,
+                                                   // a multiple of NHU (static_assert above)
+        using SL = X6Slices<HC, (HC + NHU - 1) % NHU, (HC + GU) % NHU>;
         const int u = g * GU + it;
         const int bu = std::min(u + GU, nunits - 1);
-        const uint4* src = ring + ((GP * GU + it) * 3) * NE;
-        constexpr int P0 = (GU == 2) ? 0 : GP;   // parity of the group's first unit
-        if ((P0 + it) & 1)
-          step(std::true_type{}, src, acc2[1], acc2[0], u, u - 1, u > 0, bu, GP ^ 1, it);
-        else
-          step(std::true_type{}, src, acc2[0], acc2[1], u, u - 1, u > 0, bu, GP ^ 1, it);
-      }
+        step(std::true_type{}, SL{}, ring + ((GP * GU + it) * 3) * NE, u, u - 1, u > 0, bu, GP ^ 1, it);
+      };
+      one(std::integral_constant<int, 0>{});
+      if constexpr (GU == 2) one(std::integral_constant<int, 1>{});
       if (!(NAIS_X6N_ABL & 16)) __syncthreads();
     };
     for (int g = 0; g < ngroups; g += 2) {
@@ -1788,10 +1820,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
     const int last = ngroups * GU - 1;   // the last step's unit
     if (last == nunits - 1) {            // drain: the epilogue of the chunk's last unit, no MFMAs
-      if (last & 1)
-        step(std::false_type{}, ring, acc2[0], acc2[1], last, last, true, 0, 0, 0);
-      else
-        step(std::false_type{}, ring, acc2[1], acc2[0], last, last, true, 0, 0, 0);
+      step(std::false_type{}, X6Slices<0, NHU - 1, 0>{}, ring, last, last, true, 0, 0, 0);
     }
   }
   if (tab.e) return;
