@@ -774,6 +774,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
 
     elapsed, per = run(a.precision, a.warmup, a.steps)
     wall_ms = last["wall_ms"]
+    head_out = last["out"]   # the legs below overwrite last["out"]
     ranks = None
     if world > 1:   # every rank's phase busy times (ms per step), gathered over the same group
         ph = ("table", "gather", "allgather", "merge", "topk")
@@ -950,7 +951,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                               for d in (64, 128)}
     check = None
     if emulate == 1 and not a.no_self_check and rank == 0:   # N > 1: the merged top-k
-        ids, sc = (t.cpu().numpy() for t in last["out"])
+        ids, sc = (t.cpu().numpy() for t in head_out)
         # 8 users spread over h through the torch-CPU restatement, user 1 through the numpy oracle
         check = merge_checks(self_check(p_host, data, [1], ids, sc, K),
                              self_check(p_host, data, spread_users(hist_len, 8), ids, sc, K,

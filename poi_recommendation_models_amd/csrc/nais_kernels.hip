@@ -1442,8 +1442,8 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 #ifndef NAIS_X6N_BPOS
 #define NAIS_X6N_BPOS -1
 #endif
-#ifndef NAIS_X6N_PREF
-#define NAIS_X6N_PREF 1
+#ifndef NAIS_X6N_SGB
+#define NAIS_X6N_SGB 0
 #endif
 // compile-time hidden slices of one x6n step: the unit it multiplies, the unit it finishes and the
 // unit it builds
@@ -1698,6 +1698,16 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (!(NAIS_X6N_ABL & 2) && g == (NAIS_X6N_BPOS < 0 ? NG - 1 : NAIS_X6N_BPOS * NG / 4))
           build(bu, std::integral_constant<int, HB>{}, bgrp, bit);   // a unit of the next group
       }
+#if NAIS_X6N_SGB
+      if (MMA) {   // issue order of the group: the next group's A reads, then MFMAs with VALU between
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, NAIS_X6N_SGB, 0);
+        }
+      }
+#endif
       if (s != EG || NAIS_X6N_ABL & 1) continue;
       if (m == 0) {   // the previous unit's last block, then that unit is complete
         float ap0 = apc0, ap1 = apc1;
