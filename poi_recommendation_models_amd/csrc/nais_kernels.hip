@@ -1439,11 +1439,11 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 #ifndef NAIS_X6N_ABL
 #define NAIS_X6N_ABL 0
 #endif
-#ifndef NAIS_X6N_BPOS
-#define NAIS_X6N_BPOS -1
+#ifndef NAIS_X6N_BPOS   // the next unit's build at group BPOS * NG / 4 of a step (-1: the last)
+#define NAIS_X6N_BPOS 2    // middle: D = H = 128 block 7.60 -> 7.45 ms, D = 64 unchanged (r4/ab6)
 #endif
-#ifndef NAIS_X6N_SGB
-#define NAIS_X6N_SGB 0
+#ifndef NAIS_X6N_SGB       // VALU per MFMA slot of the D = 128 issue pattern (0: none)
+#define NAIS_X6N_SGB 1
 #endif
 // compile-time hidden slices of one x6n step: the unit it multiplies, the unit it finishes and the
 // unit it builds
@@ -1698,16 +1698,17 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (!(NAIS_X6N_ABL & 2) && g == (NAIS_X6N_BPOS < 0 ? NG - 1 : NAIS_X6N_BPOS * NG / 4))
           build(bu, std::integral_constant<int, HB>{}, bgrp, bit);   // a unit of the next group
       }
-#if NAIS_X6N_SGB
-      if (MMA) {   // issue order of the group: the next group's A reads, then MFMAs with VALU between
-        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      if constexpr (D == 128 && NAIS_X6N_SGB > 0) {
+        // issue order of the group: the next group's A reads, then MFMAs with VALU between
+        // (D = H = 128 block 7.60 -> 7.46 ms; at D = 64 it costs 5 %, profiles/r4/ab6)
+        if (MMA) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
+          if (!MMA) break;
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, NAIS_X6N_SGB, 0);
         }
       }
-#endif
       if (s != EG || NAIS_X6N_ABL & 1) continue;
       if (m == 0) {   // the previous unit's last block, then that unit is complete
         float ap0 = apc0, ap1 = apc1;
