@@ -33,9 +33,10 @@ with open(os.path.join(dst, "pmc_by_kernel.csv"), "w", newline="") as fh:
     for (kern, ctr), (r0, v) in sorted(agg.items()):
         w.writerow([kern, ctr, len(v), sum(v) / len(v), min(v), max(v), r0["wg"], r0["lds"], r0["vgpr"]])
 out = {}
-# the headline table kernel: basic variant, 8 waves, fp16x6 (3 pieces) -- the fp32 / fp16x3 /
+# the headline table kernel: basic variant, D = H = 64, fp16x6 -- the fp32 / fp16x3 /
 # region_distance legs' table launches are other instantiations and stay out of the mean
-TABLE = {"fp16x6": "catalog_score_x3b_kernel<32, 2, 0, 8, 3>", "fp16x3": "catalog_score_x3b_kernel<32, 2, 0, 8, 2>"}
+TABLE = {"fp16x6": "catalog_score_x6n_kernel<64, 4, 1, false>",   # round 4: the 16x16x32 form
+         "fp16x3": "catalog_score_x3b_kernel<32, 2, 0, 8, 2>"}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
                  (TABLE.get(precision, "catalog"), "pairs_table_" + precision), ("gather_rows", "gather_rows")):
     sel = [r for r in rows if tag in r["kernel"]]
