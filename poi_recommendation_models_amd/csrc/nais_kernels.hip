@@ -1442,6 +1442,9 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 #ifndef NAIS_X6N_BPOS   // the next unit's build at group BPOS * NG / 4 of a step (-1: the last)
 #define NAIS_X6N_BPOS 2    // middle: D = H = 128 block 7.60 -> 7.45 ms, D = 64 unchanged (r4/ab6)
 #endif
+#ifndef NAIS_X6N_MB128     // hidden blocks per unit at D = 128 (2: units of 32 hidden units)
+#define NAIS_X6N_MB128 4
+#endif
 #ifndef NAIS_X6N_SGB       // VALU per MFMA slot of the D = 128 issue pattern (0: none)
 #define NAIS_X6N_SGB 1
 #endif
@@ -1582,7 +1585,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
   // of the block size (the D = 64 / 128 shapes) it has no branch, so the scheduler can spread it
   // between the MFMAs of the step it is called from.
-  auto build = [&](int u, auto hsc, int grp_, int it) {
+  auto build = [&](int u, auto hsc, int grp_, int it) __attribute__((always_inline)) {
     constexpr int HS = decltype(hsc)::value;   // the unit's hidden slice (u % NHU where it matters)
     const float* hr = hrows + (u / NHU) * D;
     uint4* dst = ring + ((grp_ * GU + it) * 3) * NE;
@@ -1611,7 +1614,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // selects, and the table rows are written by buffer stores whose offset is out of range (the
   // store dropped) for the lanes that do not write -- so the tail stays in the step's basic block.
   const uint32_t tab_bytes = tab.e ? (uint32_t)(tab.cols * 4) : 0u;
-  auto tail = [&](int pj, float p0, float p1, bool live) {
+  auto tail = [&](int pj, float p0, float p1, bool live) __attribute__((always_inline)) {
     const auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
     const float q = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);   // groups {g, g + 2}
     const auto r2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(q), __float_as_uint(q), false, false);
@@ -1642,7 +1645,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   static_assert(MB % 2 == 0, "x6n: block parity is compile-time");
   floatx4 acc[2][2];
   float apc0 = 0.f, apc1 = 0.f;
-  auto epi = [&](const float* ewb, const floatx4 (&a)[2], float& t0, float& t1) {
+  auto epi = [&](const float* ewb, const floatx4 (&a)[2], float& t0, float& t1) __attribute__((always_inline)) {
     const float4 w4 = *reinterpret_cast<const float4*>(ewb + 4 * grp);
     t0 = __builtin_fmaf(w4.x, relu_bits(a[0][0]), t0);
     t0 = __builtin_fmaf(w4.y, relu_bits(a[0][1]), t0);
@@ -1654,7 +1657,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     t1 = __builtin_fmaf(w4.w, relu_bits(a[1][3]), t1);
   };
   auto step = [&](auto do_mma, auto sl, const uint4* src, int cur, int prev, bool live, int bu, int bgrp,
-                  int bit) {
+                  int bit) __attribute__((always_inline)) {
     constexpr bool MMA = decltype(do_mma)::value;
     constexpr int HC = decltype(sl)::cur, HPV = decltype(sl)::prev, HB = decltype(sl)::built;
     constexpr int NG = KS * MB;                 // (m, s) groups of 12 MFMAs
@@ -1663,7 +1666,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const float* ewc = ew + HPU * HC;
     const float* ewp = ew + HPU * HPV + 16 * (MB - 1);
     (void)cur;
-    auto aload = [&](int g, half8 (&a)[3]) {
+    auto aload = [&](int g, half8 (&a)[3]) __attribute__((always_inline)) {
       const int m = g / KS, s = g % KS;
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -1810,9 +1813,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // clamped copy nobody reads) and finishing the previous unit; groups go in pairs, so every
     // step's hidden slices are compile-time. With GU = 2 and an odd unit count the last step runs
     // on a stale slot: only its finish of the unit before it is used.
-    auto group = [&](int g, auto gpar) {
+    auto group = [&](int g, auto gpar) __attribute__((always_inline)) {
       constexpr int GP = decltype(gpar)::value;
-      auto one = [&](auto itc) {
+      auto one = [&](auto itc) __attribute__((always_inline)) {
         constexpr int it = decltype(itc)::value;
         constexpr int HC = (GP * GU + it) % NHU;   // u % NHU: a group pair spans 2 GU units,
                                                    // a multiple of NHU (static_assert above)
@@ -2559,11 +2562,11 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
                        hipStream_t stream, const TableOut& tab = TableOut{}) {
   if constexpr (NPC == 3 && !VarT<VAR>::DIST && (DH == 16 || DH == 32 || DH == 64)) {
     if (x6n_enabled()) {
-      // D <= 64: one unit up to 64 hidden units, two at H = 128; D = 128: units of 32 hidden
-      // units (MB = 4 would need more than the 256 VGPRs of two waves per SIMD)
+      // one unit up to 64 hidden units, two at H = 128 (D = 128 with 32-hidden units, MB = 2:
+      // 1 % slower in the same process, profiles/r4/ab8)
       constexpr int D = 2 * DH;
-      constexpr int MB = D == 128 ? 2 : (HB <= 2 ? 2 * HB : 4);
-      constexpr int NHU = D == 128 ? HB : (HB <= 2 ? 1 : 2);
+      constexpr int MB = (D == 128 && NAIS_X6N_MB128 == 2) ? 2 : (HB <= 2 ? 2 * HB : 4);
+      constexpr int NHU = (D == 128 && NAIS_X6N_MB128 == 2) ? HB : (HB <= 2 ? 1 : 2);
       constexpr bool REG = VarT<VAR>::REGION;
       using CN = CfgN<D, MB, NHU>;
       const size_t lds = CN::BYTES;
