@@ -229,6 +229,8 @@ def test_region_validation_dropin_metrics(precision):
 @pytest.mark.parametrize("variant,D,H", [
     ("basic", 8, 16), ("basic", 16, 16), ("basic", 32, 48), ("basic", 64, 64), ("basic", 128, 128),
     ("basic", 64, 128), ("basic", 128, 64), ("basic", 64, 20),
+    # every x6n unit shape (D in {32, 64, 128} x MB in {2, 4} x NHU in {1, 2}), padded hidden rows
+    ("basic", 128, 32), ("basic", 128, 96), ("basic", 32, 128), ("region", 128, 64), ("region", 64, 128),
     ("region", 16, 32), ("region", 64, 64), ("region", 128, 128),
     ("region_distance", 16, 32), ("region_distance", 64, 64), ("region_distance", 128, 96),
     ("distance", 16, 16), ("distance", 64, 64), ("distance", 128, 128),
@@ -241,6 +243,7 @@ def test_catalog_vs_oracle_shapes(variant, D, H, precision):
 @pytest.mark.parametrize("variant,D,H", [
     ("basic", 16, 16), ("basic", 64, 64), ("basic", 128, 128), ("region", 64, 64),
     ("region_distance", 64, 64), ("distance", 64, 64),
+    ("basic", 128, 64), ("basic", 32, 32), ("basic", 32, 128), ("region", 128, 128),
 ])
 def test_catalog_pairs_vs_oracle_shapes(variant, D, H, precision):
     _catalog_vs_oracle(variant, D, H, precision, "pairs")
