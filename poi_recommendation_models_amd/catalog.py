@@ -251,6 +251,10 @@ PAIR_CU_LAYOUT = "contiguous"   # or "interleaved" (kept for the A/B)
 # bound by the memory side, not by their CUs -- at 0 / 0.04 / 0.08 / 0.12 the job took 545.4 /
 # 542.6 / 552.6 / 614.8 ms while the gather stream's own time fell only 539 -> 532 ms
 # (profiles/r1/table_gather_frac/; results bit-identical, test_pairs_blocks_passes_bit_identical).
+# Round 4 (the 16x16x32 tables now the faster stream at config 4): 0 / 0.03 / 0.05 / 0.08 ->
+# 604 / 599 / 594 / 609 ms on one box (profiles/r4/tgf), but 0.05 on a box whose tables ran at
+# 601 ms made the table stream the bound (607 ms, profiles/r4/tgf2): box to box the two streams
+# trade places, so the share stays 0.
 PAIR_TABLE_GATHER_FRAC = 0.0
 # Table launches alternate over two streams with the same CU mask, so block b + 1's workgroups
 # fill the CUs that block b's last, partial round of workgroups leaves idle (1,564 workgroups of
