@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 9
+#define NAIS_ABI_VERSION 10
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -218,6 +218,13 @@ int32_t nais_gather_rows(const float* table, int64_t rows, int32_t dim,
  *                      scores, 0 for full rows); NaNs counted into *nan_count as
  *                      nais_score_catalog does.
  * The caller loops over column blocks sized to its memory budget and runs nais_topk_rows.
+ *   work (nais_pair_table, nais_pair_gather_topk; may be NULL): one int32 of device memory private
+ *                      to the stream. Given, the launch runs as a work queue -- about one
+ *                      resident round of workgroups takes (item group, column tile) or user slots
+ *                      from this counter (zeroed by the call, stream-ordered) until they run out,
+ *                      so a CU-masked stream whose CU count is not a multiple of the shader-engine
+ *                      count still uses every CU (nais_pair_table: the 16x16x32 fp16x6 kernel
+ *                      only; other shapes ignore it). Results are identical either way.
  *   nais_pair_gather_topk  the same sums and scores, but instead of score rows each user keeps a
  *                      running top-k: keys[slot*k ..] (uint64, sorted descending, kcount[slot]
  *                      valid; zero kcount before the first call) with key = ordered(score) << 32 |
@@ -234,7 +241,7 @@ int32_t nais_pair_rows(const int64_t* indptr, const int64_t* indices, const int3
 int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
                         int64_t col0, int64_t cols, const int64_t* region_of,
                         const double* coords, const double* latlon_mat, float* e, float* es,
-                        int64_t ld, void* stream);
+                        int64_t ld, int32_t* work, void* stream);
 int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
                          const int64_t* indptr, const int64_t* indices, const int32_t* users,
                          int32_t num_users, int64_t col0, int64_t cols, float beta, float* scores,
@@ -242,7 +249,8 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
 int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
-                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, void* stream);
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* work,
+                              void* stream);
 int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,
                               int32_t* out_ids, float* out_scores, int32_t* short_count, void* stream);
 /*

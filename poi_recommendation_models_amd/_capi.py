@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
@@ -202,13 +202,13 @@ def load(path: str | None = None):
     lib.nais_pair_rows.argtypes = [vp, vp, vp, i32, i64, vp, vp, vp, vp, sz, vp]
     lib.nais_pair_table.restype = i32
     lib.nais_pair_table.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp, vp,
-                                    i64, vp]
+                                    i64, vp, vp]
     lib.nais_pair_gather.restype = i32
     lib.nais_pair_gather.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, vp, i64, i64, vp,
                                      vp]
     lib.nais_pair_gather_topk.restype = i32
     lib.nais_pair_gather_topk.argtypes = [vp, vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp,
-                                          vp]
+                                          vp, vp]
     lib.nais_pair_prior_table.restype = i32
     lib.nais_pair_prior_table.argtypes = [vp, i64, vp, i64, i64, i64, f64, f64, vp, i64, vp]
     lib.nais_pair_prior_gather.restype = i32

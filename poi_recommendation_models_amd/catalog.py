@@ -260,10 +260,15 @@ PAIR_TABLE_GATHER_FRAC = 0.0
 # fill the CUs that block b's last, partial round of workgroups leaves idle (1,564 workgroups of
 # one table block = 9.8 rounds over 160 CUs; one stream waits for the whole launch to drain).
 PAIR_TABLE_STREAMS = int(os.environ.get("NAIS_PAIR_TABLE_STREAMS", "2"))
+# Work-queue launches of the table (16x16x32 kernel) and fused-gather kernels (round 4): a resident
+# round of workgroups takes items from a counter, so a stream's CU count need not be a multiple of
+# the 32 shader engines (auto_table_cus then steps in PAIR_SPLIT_STEP CUs).
+PAIR_WORK_QUEUE = os.environ.get("NAIS_PAIR_WORK_QUEUE", "1") != "0"
+PAIR_SPLIT_STEP = 8
 _masked: dict = {}
 
 
-def auto_table_cus(model, J, NC, entries, ncu, prior=False):
+def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/, re-fitted in round 3 on the fp16x6 tables:
@@ -277,15 +282,28 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False):
     H, din = model.attn_layer1.weight.shape
     prec = getattr(model, "precision", "fp16x6")
     products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
-    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else 1.25e15)
     gbytes = entries * NC * 8.0
     if prior:
-        t_tab += J * NC * 1.4e-11
         gbytes *= 2
     xcd = max(1, ncu // 8)
+    # with work-queue launches the split may step finer than a CU per shader engine (x6n tables
+    # and the fused gather; other table kernels keep the engine-sized steps)
+    x6n = (PAIR_WORK_QUEUE and products == 6 and din in (32, 64, 128) and not prior)
+    step = min(PAIR_SPLIT_STEP, xcd) if x6n else xcd
+    rate = 1.5e15 if x6n else 1.25e15   # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard)
+    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else rate)
+    if prior:
+        t_tab += J * NC * 1.4e-11
+    # gather rate per CU: ~72 GB/s while a block's e / e*s tables (block_bytes) mostly stay in the
+    # 256 MB Infinity Cache (config 4: 410 MB), ~51 GB/s from HBM (config-5 shard: 4.1 GB; round 4,
+    # 1.64 TB/s on 32 CUs)
+    per_cu = 72e9 if block_bytes is None or block_bytes <= 512e6 else 51e9
+    # the memory side's cap for the gather beside running tables: 7.5 TB/s alone, ~6.8 beside the
+    # x6n tables (round 4: 96 -> 104 gather CUs at config 4 read no faster, 600 -> 627 ms)
+    cap = 6.8e12 if x6n else 7.5e12
     best, best_t = ncu // 2, None
-    for n in range(ncu // 4, ncu - xcd + 1, xcd):
-        t = max(t_tab * ncu / n, gbytes / min(7.5e12, (ncu - n) * 72e9))
+    for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
+        t = max(t_tab * ncu / n, gbytes / min(cap, (ncu - n) * per_cu))
         if best_t is None or t <= best_t:   # ties (gather-bound): the larger table share
             best, best_t = n, t
     return best
@@ -420,9 +438,23 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         prior_flags = _capi.PRIOR_FINITE if _prior_entries_finite(pa, pb) else 0
     pr_of = {}   # column-block table -> its float64 pr_d table (prior only)
 
+    # work-queue counters (PAIR_WORK_QUEUE): one int32 per stream, each used stream-ordered; on
+    # only for a split off the shader-engine steps (at them the classic grids measured as fast)
+    wq_slots = torch.zeros(8, dtype=torch.int32, device=dev) if PAIR_WORK_QUEUE else None
+    wq_of = {}
+    wq_on = [False]
+
+    def wq(stream_):
+        if wq_slots is None or not wq_on[0]:
+            return None
+        h = int(stream_ or 0)
+        if h not in wq_of:
+            wq_of[h] = wq_slots.data_ptr() + 4 * len(wq_of)
+        return wq_of[h]
+
     def table(tab, c0, w, stream_):
         model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
-                          tab[1].data_ptr(), ld, stream_)
+                          tab[1].data_ptr(), ld, stream_, work=wq(stream_))
         if prior is not None:
             _capi.check(lib.nais_pair_prior_table(pri_coords.data_ptr(), P, items.data_ptr(), J, c0, w,
                                                   float(pa), float(pb), pr_of[id(tab)].data_ptr(), ld,
@@ -462,7 +494,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta), k,
                     keys.data_ptr() + 8 * k * a, kcount.data_ptr() + 4 * a, counters[0:1].data_ptr(),
-                    stream_), "nais_pair_gather_topk")
+                    wq(stream_), stream_), "nais_pair_gather_topk")
         else:
             scores = torch.empty(m, NC, dtype=torch.float32, device=dev)
             if prior is not None:
@@ -488,8 +520,9 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             ld = (W + 3) // 4 * 4
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None) if PAIR_TABLE_CUS < 0
-                         else PAIR_TABLE_CUS)
+            table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None, J * ld * 8)
+                         if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS)
+            wq_on[0] = table_cus % max(1, ncu // 8) != 0
             if events is not None:
                 events.append(("table_cus", None, None, table_cus))
                 events.append(("block_cols", None, None, W))
@@ -558,8 +591,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 torch_stream.wait_stream(gs)
                 for t_ in tss:
                     torch_stream.wait_stream(t_)
-                for t in [*tabs, *pr_of.values()]:   # not handed to the main stream early
-                    for t_ in (*tss, gs):
+                for t in [*tabs, *pr_of.values(), *([wq_slots] if wq_slots is not None else [])]:
+                    for t_ in (*tss, gs):   # not handed to the main stream early
                         t.record_stream(t_)
             del tabs
             pr_of.clear()

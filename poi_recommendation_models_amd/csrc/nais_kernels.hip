@@ -71,6 +71,9 @@ struct TableOut {
   float* es = nullptr;
   int64_t ld = 0, col0 = 0, cols = 0, nitems = 0;
   int32_t gi = 0;
+  // work queue (x6n only): the launch's item counter, zeroed before it, and the item grid it covers
+  int32_t* work = nullptr;
+  int32_t ngroups = 0, ntiles = 0;
 };
 // the pair's two terms for item row `row` (relative to the launch's base) and column offset x
 __device__ __forceinline__ void tab_put(const TableOut& t, int64_t row, int64_t x, float e, float es) {
@@ -1495,21 +1498,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* svt = reinterpret_cast<float*>(hid + JCB);                // per wave [32 cands][SVP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = lane >> 4, l16 = lane & 15;
-  int64_t hbeg, hlen;
-  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
-    hbeg = (int64_t)cat_user_slot() * tab.gi;
-    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
-  } else {
-    const int64_t u = users[cat_user_slot()];
-    hbeg = indptr[u];
-    hlen = indptr[u + 1] - hbeg;
-  }
-  const int64_t cbase = tab.col0 + (int64_t)cat_tile() * CPB + wave * 32;
   const int64_t clim = tab.e ? std::min<int64_t>(p.P, tab.col0 + tab.cols) : p.P;
-  // after the lane-group reduction lane L holds candidate cbase + 16 (L >> 5) + (L & 15) (L and
-  // L ^ 16 alike): lane groups 0 / 2 carry e, groups 1 / 3 e * s
-  const int64_t cout = cbase + 16 * (lane >> 5) + l16;
-  const bool vout = cout < clim;
 
   // ---- this thread's W1 values for its build entries of every unit (fp32, unscaled)
   float wv[NHU][EPT][8];
@@ -1533,42 +1522,82 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   }
   const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg
 
-  // ---- candidate operands: two blocks of 16, one scale S_t per wave, split into B fragments
+  float SAcur = 1.f;   // the W1 registers' current scale (rescaled per chunk)
+
+  // Work items: (item group, column tile) in pair-table mode, (user slot, column tile) otherwise.
+  // With tab.work (pair-table mode) the workgroup takes items from that counter until they run
+  // out -- a work queue, so a shader engine with fewer enabled CUs simply takes fewer (the stream
+  // split needs no 32-CU steps); items are tile-major, so a workgroup's candidate operands usually
+  // carry over to its next item.
+  __shared__ int32_t wi_sh;
+  int64_t wslot = cat_user_slot(), wtile = cat_tile(), cur_tile = -1;
   half8 tb[2][KS][3];
-  float St;
-  {
-    float tmax = 0.f;
+  float St = 1.f;
+  int64_t cbase = 0, cout = 0;
+  bool vout = false;
+  for (int64_t it = 0;; ++it) {
+  if (tab.work) {
+    __syncthreads();   // the previous item's readers of wi_sh, hrows, hid and the ring are done
+    if (tid == 0) wi_sh = atomicAdd(tab.work, 1);
+    __syncthreads();
+    const int64_t wi = wi_sh;
+    if (wi >= (int64_t)tab.ngroups * tab.ntiles) break;
+    wtile = wi / tab.ngroups;
+    wslot = wi % tab.ngroups;
+  } else if (it > 0) {
+    break;
+  }
+  int64_t hbeg, hlen;
+  if (tab.e) {   // pair-table mode: a group of tab.gi rows of the item list
+    hbeg = wslot * tab.gi;
+    hlen = std::min<int64_t>(tab.gi, tab.nitems - hbeg);
+  } else {
+    const int64_t u = users[wslot];
+    hbeg = indptr[u];
+    hlen = indptr[u + 1] - hbeg;
+  }
+  if (wtile != cur_tile) {   // block-uniform
+    cur_tile = wtile;
+    cbase = tab.col0 + wtile * CPB + wave * 32;
+    // after the lane-group reduction lane L holds candidate cbase + 16 (L >> 5) + (L & 15) (L and
+    // L ^ 16 alike): lane groups 0 / 2 carry e, groups 1 / 3 e * s
+    cout = cbase + 16 * (lane >> 5) + l16;
+    vout = cout < clim;
+    // ---- candidate operands: two blocks of 16, one scale S_t per wave, split into B fragments
+    {
+      float tmax = 0.f;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int64_t c = cbase + 16 * nb + l16;
-      const int64_t cc = c < clim ? c : p.P - 1;
+      for (int nb = 0; nb < 2; ++nb) {
+        const int64_t c = cbase + 16 * nb + l16;
+        const int64_t cc = c < clim ? c : p.P - 1;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int k0 = 32 * s + 8 * grp;
-        const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
-                                                : p.et + cc * p.item_dim + k0;
-        const float4 v0 = reinterpret_cast<const float4*>(src)[0];
-        const float4 v1 = reinterpret_cast<const float4*>(src)[1];
-        tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
-                                 fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)))));
+        for (int s = 0; s < KS; ++s) {
+          const int k0 = 32 * s + 8 * grp;
+          const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
+                                                  : p.et + cc * p.item_dim + k0;
+          const float4 v0 = reinterpret_cast<const float4*>(src)[0];
+          const float4 v1 = reinterpret_cast<const float4*>(src)[1];
+          tmax = fmaxf(tmax, fmaxf(fmaxf(fmaxf(fabsf(v0.x), fabsf(v0.y)), fmaxf(fabsf(v0.z), fabsf(v0.w))),
+                                   fmaxf(fmaxf(fabsf(v1.x), fabsf(v1.y)), fmaxf(fabsf(v1.z), fabsf(v1.w)))));
+        }
       }
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
-    St = pow2_scale(tmax);
+      for (int o = 32; o > 0; o >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, o));
+      St = pow2_scale(tmax);
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {   // second read of the rows (L1 / L2 hits): fewer live VGPRs
-      const int64_t c = cbase + 16 * nb + l16;
-      const int64_t cc = c < clim ? c : p.P - 1;
+      for (int nb = 0; nb < 2; ++nb) {   // second read of the rows (L1 / L2 hits): fewer live VGPRs
+        const int64_t c = cbase + 16 * nb + l16;
+        const int64_t cc = c < clim ? c : p.P - 1;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int k0 = 32 * s + 8 * grp;
-        const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
-                                                : p.et + cc * p.item_dim + k0;
-        const float4 v0 = reinterpret_cast<const float4*>(src)[0];
-        const float4 v1 = reinterpret_cast<const float4*>(src)[1];
-        float x[8] = {v0.x * St, v0.y * St, v0.z * St, v0.w * St, v1.x * St, v1.y * St, v1.z * St, v1.w * St};
-        split_pieces<3>(x, tb[nb][s]);
+        for (int s = 0; s < KS; ++s) {
+          const int k0 = 32 * s + 8 * grp;
+          const float* src = (REGION && k0 >= DH) ? p.er + region_of[cc] * p.region_dim + (k0 - DH)
+                                                  : p.et + cc * p.item_dim + k0;
+          const float4 v0 = reinterpret_cast<const float4*>(src)[0];
+          const float4 v1 = reinterpret_cast<const float4*>(src)[1];
+          float x[8] = {v0.x * St, v0.y * St, v0.z * St, v0.w * St, v1.x * St, v1.y * St, v1.z * St, v1.w * St};
+          split_pieces<3>(x, tb[nb][s]);
+        }
       }
     }
   }
@@ -1578,7 +1607,6 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   const float* eb = Escl + wave * EPI;        // S*b1 by hidden unit
   const float* ew = eb + HP;                  // w2/S
   float* sv_mine = svt + wave * 32 * SVP;
-  float SAcur = 1.f;
   int64_t j0 = 0;
   float pa0 = 0.f, pa1 = 0.f;                 // logit partials of the item's earlier units
 
@@ -1837,18 +1865,19 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       step(std::false_type{}, X6Slices<0, NHU - 1, 0>{}, ring, last, last, true, 0, 0, 0);
     }
   }
-  if (tab.e) return;
-
-  const float logit = finish_logit(S, N, p.beta, hlen == 0);
-  const bool isnan_ = logit != logit;
-  float sc = sigmoidf_ref(logit);
-  if (isnan_) sc = __builtin_nanf("");
-  if (in_hist) sc = -1.f;
-  const bool writer = vout && !(grp & 1);
-  if (writer) scores[(int64_t)cat_user_slot() * score_ld + cout] = sc;
-  if (nan_count) {
-    const unsigned long long m = __ballot(writer && !in_hist && isnan_);
-    if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+  if (!tab.e) {
+    const float logit = finish_logit(S, N, p.beta, hlen == 0);
+    const bool isnan_ = logit != logit;
+    float sc = sigmoidf_ref(logit);
+    if (isnan_) sc = __builtin_nanf("");
+    if (in_hist) sc = -1.f;
+    const bool writer = vout && !(grp & 1);
+    if (writer) scores[wslot * score_ld + cout] = sc;
+    if (nan_count) {
+      const unsigned long long m = __ballot(writer && !in_hist && isnan_);
+      if (lane == 0 && m) atomicAdd(nan_count, (int32_t)__popcll(m));
+    }
+  }
   }
 }
 
@@ -2578,8 +2607,22 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
         attr_set = true;
       }
       dim3 grid = tab.e ? table_grid(tab, nb, CN::CPB) : cat_grid(d.P, nb, CN::CPB);
+      TableOut t = tab;
+      if (t.e && t.work) {   // work queue: one workgroup per CU (the LDS holds one), items tile-major
+        t.ngroups = (int32_t)grid.y;
+        t.ntiles = (int32_t)grid.x;
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+          return fail(NAIS_E_HIP, "device attributes");
+        grid = dim3((unsigned)std::min<int64_t>((int64_t)grid.x * grid.y, ncu), 1, 1);
+        if (hipMemsetAsync(t.work, 0, sizeof(int32_t), stream) != hipSuccess)
+          return fail(NAIS_E_HIP, "hipMemsetAsync(work)");
+      } else {
+        t.work = nullptr;
+      }
       hipLaunchKernelGGL(kern, grid, dim3(CN::THREADS), lds, stream, d, indptr, indices, users,
-                         region_of, scores, ld, nan_count, tab);
+                         region_of, scores, ld, nan_count, t);
       return check_launch("catalog_score_x6n_kernel");
     }
   }
@@ -2822,7 +2865,8 @@ namespace {
 // nais_pair_table: two row-major tables (e, es) with row pitch ld
 int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64_t num_items,
                         int64_t col0, int64_t cols, const int64_t* region_of, const double* coords,
-                        const double* latlon_mat, float* e, float* es, int64_t ld, void* stream) {
+                        const double* latlon_mat, float* e, float* es, int64_t ld, int32_t* work,
+                        void* stream) {
   Shape sh;
   int rc = validate(params, &sh);
   if (rc) return rc;
@@ -2845,6 +2889,7 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
   tab.ld = ld;
   tab.cols = cols;
   tab.gi = PAIR_GROUP_ITEMS;
+  tab.work = work;
   const int64_t groups_per_launch = 65535;
   for (int64_t g0 = 0; g0 * tab.gi < num_items; g0 += groups_per_launch) {
     const int64_t base = g0 * tab.gi;
@@ -2872,9 +2917,9 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
 int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64_t num_items,
                         int64_t col0, int64_t cols, const int64_t* region_of,
                         const double* coords, const double* latlon_mat, float* e, float* es,
-                        int64_t ld, void* stream) {
+                        int64_t ld, int32_t* work, void* stream) {
   return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, e, es,
-                         ld, stream);
+                         ld, work, stream);
 }
 
 int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,

@@ -274,12 +274,29 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
                         const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
                         int32_t nusers, int64_t col0, int64_t cols, float beta, int k,
                         unsigned long long* __restrict__ keys, int32_t* __restrict__ kcount,
-                        int32_t* __restrict__ nan_count) {
+                        int32_t* __restrict__ nan_count, int32_t* __restrict__ work) {
   __shared__ unsigned long long lk[GW][TK_LDS];
   __shared__ uint32_t hm[GW][STRIPE / 32];   // history POIs of this stripe, one bit per column
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t slot = int64_t(blockIdx.x) * GW + w;
-  if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
+  // work != null: a work queue -- every wave takes user slots from the counter until they run out,
+  // so a shader engine with fewer enabled CUs takes fewer (no 32-CU steps in the stream split)
+  constexpr int GQ = 4;   // slots per grab: a quarter of the atomics on the one counter
+  int64_t qnext = 0, qend = 0;
+  for (int64_t it = 0;; ++it) {
+  int64_t slot;
+  if (work) {
+    if (qnext == qend) {
+      int got = 0;
+      if (lane == 0) got = atomicAdd(work, GQ);
+      qnext = __builtin_amdgcn_readfirstlane(got);
+      qend = qnext + GQ;
+    }
+    slot = qnext++;
+  } else {
+    if (it > 0) break;
+    slot = int64_t(blockIdx.x) * GW + w;
+  }
+  if (slot >= nusers) break;                 // wave-uniform; no workgroup barriers below
   const int64_t u = users[slot];
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int64_t x = int64_t(lane) * CPL;     // column within the stripe [col0, col0 + cols)
@@ -338,7 +355,7 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
   }
   const int m = __shfl(excl, 63);
   excl -= mine_n;
-  if (m == 0) return;
+  if (m == 0) continue;
   unsigned long long* L = lk[w];
   for (int i = lane; i < cnt; i += 64) L[i] = keys[slot * k + i];
   int pos = cnt + excl;
@@ -370,6 +387,8 @@ pair_gather_topk_kernel(const float* __restrict__ E, const float* __restrict__ E
   const int nk = n < k ? n : k;
   for (int i = lane; i < nk; i += 64) keys[slot * k + i] = L[i];
   if (lane == 0) kcount[slot] = nk;
+  wave_lds_sync();   // the next slot's hm / lk writers after this slot's readers
+  }
 }
 
 
@@ -575,7 +594,8 @@ int32_t nais_pair_gather(const float* e, const float* es, int64_t ld, const int3
 int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const int32_t* rowmap,
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
-                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, void* stream) {
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* work,
+                              void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || k <= 0)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
   if (k > TK_LDS - STRIPE) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
@@ -585,12 +605,21 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
     return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
   if (ld % 4 != 0) return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const unsigned groups = (unsigned)((num_users + GW - 1) / GW);
+  unsigned groups = (unsigned)((num_users + GW - 1) / GW);
+  if (work) {   // a work queue: about one resident round of workgroups (5 per CU at 81 VGPRs)
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      return nais_internal_fail(NAIS_E_HIP, "device attributes");
+    groups = std::min<unsigned>(groups, (unsigned)ncu * 6u);
+  }
   for (int64_t s0 = 0; s0 < cols; s0 += STRIPE) {   // one launch per stripe: one writer per list
+    if (work && hipMemsetAsync(work, 0, sizeof(int32_t), st) != hipSuccess)
+      return nais_internal_fail(NAIS_E_HIP, "hipMemsetAsync(work)");
     hipLaunchKernelGGL(pair_gather_topk_kernel, dim3(groups), dim3(GW * 64), 0, st, e + s0, es + s0, ld,
                        rowmap, indptr, indices, users, num_users, col0 + s0,
                        std::min<int64_t>(STRIPE, cols - s0), beta, (int)k,
-                       reinterpret_cast<unsigned long long*>(keys), kcount, nan_count);
+                       reinterpret_cast<unsigned long long*>(keys), kcount, nan_count, work);
     const int32_t rc = nais_internal_check_launch("pair_gather_topk_kernel");
     if (rc) return rc;
   }

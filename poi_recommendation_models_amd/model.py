@@ -95,9 +95,9 @@ class _NAISDevice(nn.Module):
     # builder, a post-gather pass over the score rows, and whether the direct kernels apply
     _pairs_only = False
 
-    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream):
+    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream, work=None):
         _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg), _capi.ptr(cor),
-                                        _capi.ptr(llm), e, es, ld, stream), "nais_pair_table")
+                                        _capi.ptr(llm), e, es, ld, work, stream), "nais_pair_table")
 
     def _pair_fixup(self, csr, users, m, scores, c0, c1, stream):
         pass
@@ -916,7 +916,7 @@ class transform_attn(_NearPOIModel):
         self._last_nan = nan
         return out
 
-    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream):
+    def _pair_table(self, lib, prm, items, J, c0, w, reg, cor, llm, e, es, ld, stream, work=None):
         _capi.check(lib.nais_dot_pair_table(self.dot_tables(), items.data_ptr(), J, c0, w, e, es, ld, stream),
                     "nais_dot_pair_table")
 

@@ -84,7 +84,7 @@ def main():
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
             _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, cols, None, None, None,
-                                            tab[0].data_ptr(), tab[1].data_ptr(), W, st), "table")
+                                            tab[0].data_ptr(), tab[1].data_ptr(), W, None, st), "table")
             e[1].record()
             _capi.check(lib.nais_pair_gather(tab[0].data_ptr(), tab[1].data_ptr(), W, rowmap.data_ptr(),
                                              csr.indptr.data_ptr(), csr.indices.data_ptr(), users.data_ptr(),

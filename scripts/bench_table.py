@@ -57,7 +57,7 @@ def main():
                 c0 = (b * W) % (P - W)
                 _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, W, None, None, None,
                                                 tabs[v][0].data_ptr(), tabs[v][1].data_ptr(), W,
-                                                st.cuda_stream), "nais_pair_table")
+                                                None, st.cuda_stream), "nais_pair_table")
             e1.record(st)
             torch.cuda.synchronize(dev)
             if r > 0:
