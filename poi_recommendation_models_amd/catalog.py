@@ -298,9 +298,7 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None):
     # 256 MB Infinity Cache (config 4: 410 MB), ~51 GB/s from HBM (config-5 shard: 4.1 GB; round 4,
     # 1.64 TB/s on 32 CUs)
     per_cu = 72e9 if block_bytes is None or block_bytes <= 512e6 else 51e9
-    # the memory side's cap for the gather beside running tables: 7.5 TB/s alone, ~6.8 beside the
-    # x6n tables (round 4: 96 -> 104 gather CUs at config 4 read no faster, 600 -> 627 ms)
-    cap = 6.8e12 if x6n else 7.5e12
+    cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
         t = max(t_tab * ncu / n, gbytes / min(cap, (ncu - n) * per_cu))
@@ -439,7 +437,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     pr_of = {}   # column-block table -> its float64 pr_d table (prior only)
 
     # work-queue counters (PAIR_WORK_QUEUE): one int32 per stream, each used stream-ordered; on
-    # only for a split off the shader-engine steps (at them the classic grids measured as fast)
+    # only for a split off the shader-engine steps (config 4 at 152 / 104: 598 ms vs 607 at the
+    # classic 160 / 96; config-5 shard at 232 / 24: 17.3 s vs 18.2 at 224 / 32 -- profiles/r4/wq)
     wq_slots = torch.zeros(8, dtype=torch.int32, device=dev) if PAIR_WORK_QUEUE else None
     wq_of = {}
     wq_on = [False]

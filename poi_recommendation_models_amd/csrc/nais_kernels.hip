@@ -2608,13 +2608,11 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
       }
       dim3 grid = tab.e ? table_grid(tab, nb, CN::CPB) : cat_grid(d.P, nb, CN::CPB);
       TableOut t = tab;
-      if (t.e && t.work) {   // work queue: one workgroup per CU (the LDS holds one), items tile-major
-        t.ngroups = (int32_t)grid.y;
+      if (t.e && t.work) {   // work queue: one workgroup per CU of the stream's mask (the LDS
+        t.ngroups = (int32_t)grid.y;   // holds one), items tile-major
         t.ntiles = (int32_t)grid.x;
-        int dev = 0, ncu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-          return fail(NAIS_E_HIP, "device attributes");
+        const int ncu = nais_internal_stream_cus(stream);
+        if (ncu <= 0) return fail(NAIS_E_HIP, "device attributes");
         grid = dim3((unsigned)std::min<int64_t>((int64_t)grid.x * grid.y, ncu), 1, 1);
         if (hipMemsetAsync(t.work, 0, sizeof(int32_t), stream) != hipSuccess)
           return fail(NAIS_E_HIP, "hipMemsetAsync(work)");
@@ -2741,6 +2739,18 @@ int launch_prior(const double* coords, int64_t P, const int64_t* indptr, const i
 }  // namespace
 
 int nais_internal_fail(int code, const char* msg) { return fail(code, msg); }
+int nais_internal_stream_cus(hipStream_t stream) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    return -1;
+  uint32_t mask[32] = {};
+  const uint32_t words = (uint32_t)std::min(32, (ncu + 31) / 32);
+  if (hipExtStreamGetCUMask(stream, words, mask) != hipSuccess) return ncu;
+  int n = 0;
+  for (uint32_t i = 0; i < words; ++i) n += __builtin_popcount(mask[i]);
+  return n > 0 ? std::min(n, ncu) : ncu;
+}
 int nais_internal_check_launch(const char* what) { return check_launch(what); }
 
 extern "C" {

@@ -606,12 +606,10 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
   if (ld % 4 != 0) return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   unsigned groups = (unsigned)((num_users + GW - 1) / GW);
-  if (work) {   // a work queue: about one resident round of workgroups (5 per CU at 81 VGPRs)
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      return nais_internal_fail(NAIS_E_HIP, "device attributes");
-    groups = std::min<unsigned>(groups, (unsigned)ncu * 6u);
+  if (work) {   // a work queue: one resident round of workgroups on the stream's CUs (5 per CU)
+    const int ncu = nais_internal_stream_cus(st);
+    if (ncu <= 0) return nais_internal_fail(NAIS_E_HIP, "device attributes");
+    groups = std::min<unsigned>(groups, (unsigned)ncu * 5u);
   }
   for (int64_t s0 = 0; s0 < cols; s0 += STRIPE) {   // one launch per stripe: one writer per list
     if (work && hipMemsetAsync(work, 0, sizeof(int32_t), st) != hipSuccess)

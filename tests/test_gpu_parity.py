@@ -568,6 +568,9 @@ def test_pairs_auto_choice_and_new4():
     {"PAIR_LPT_ORDER": False, "PAIR_FUSED_TOPK": False},
     {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.1},   # tail users on the table stream
     {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_GATHER_FRAC": 0.9, "PAIR_LPT_ORDER": False},
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_CUS": 152},            # off the engine steps: work queues
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_CUS": 232, "PAIR_TABLE_STREAMS": 1},
+    {"PAIR_BLOCK_COLS": 256, "PAIR_TABLE_CUS": 152, "PAIR_WORK_QUEUE": False},
 ])
 def test_pairs_blocks_passes_bit_identical(knobs):
     """The pairs pipeline's schedule (block width, overlap on CU-masked streams or serial, the
