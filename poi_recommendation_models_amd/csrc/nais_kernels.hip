@@ -1437,20 +1437,6 @@ __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const hal
 // whose logit partials are summed before the tail. The ring holds 2 groups of GU units: GU = 2
 // where a unit is <= 24 KiB, else 1 (a whole D = H = 128 item, 96 KiB, does not fit twice in the
 // 160 KiB LDS, hence units).
-// ablations for timing only (results are garbage): 1 no epilogue, 2 no build, 4 no A-fragment LDS
-// reads, 8 no tail, 16 no group barriers
-#ifndef NAIS_X6N_ABL
-#define NAIS_X6N_ABL 0
-#endif
-#ifndef NAIS_X6N_BPOS   // the next unit's build at group BPOS * NG / 4 of a step (-1: the last)
-#define NAIS_X6N_BPOS 2    // middle: D = H = 128 block 7.60 -> 7.45 ms, D = 64 unchanged (r4/ab6)
-#endif
-#ifndef NAIS_X6N_MB128     // hidden blocks per unit at D = 128 (2: units of 32 hidden units)
-#define NAIS_X6N_MB128 4
-#endif
-#ifndef NAIS_X6N_SGB       // VALU per MFMA slot of the D = 128 issue pattern (0: none)
-#define NAIS_X6N_SGB 1
-#endif
 // compile-time hidden slices of one x6n step: the unit it multiplies, the unit it finishes and the
 // unit it builds
 template <int C, int P, int B>
@@ -1698,12 +1684,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       const int m = g / KS, s = g % KS;
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        if (NAIS_X6N_ABL & 4) {
-          a[q] = tb[1][s][q];
-        } else {
-          const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
-          a[q] = *reinterpret_cast<const half8*>(&u4);
-        }
+        const uint4 u4 = src[q * NE + (m * KS + s) * 64 + lane];
+        a[q] = *reinterpret_cast<const half8*>(&u4);
       }
     };
     half8 a_nx[3];
@@ -1726,10 +1708,11 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (g + 1 < NG) aload(g + 1, a_nx);
         acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
         acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
-        if (!(NAIS_X6N_ABL & 2) && g == (NAIS_X6N_BPOS < 0 ? NG - 1 : NAIS_X6N_BPOS * NG / 4))
-          build(bu, std::integral_constant<int, HB>{}, bgrp, bit);   // a unit of the next group
+        // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
+        // against the last group; D = 64 unchanged -- profiles/r4/ab6)
+        if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
       }
-      if constexpr (D == 128 && NAIS_X6N_SGB > 0) {
+      if constexpr (D == 128) {
         // issue order of the group: the next group's A reads, then MFMAs with VALU between
         // (D = H = 128 block 7.60 -> 7.46 ms; at D = 64 it costs 5 %, profiles/r4/ab6)
         if (MMA) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
@@ -1737,18 +1720,16 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         for (int k = 0; k < 12; ++k) {
           if (!MMA) break;
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, NAIS_X6N_SGB, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
         }
       }
-      if (s != EG || NAIS_X6N_ABL & 1) continue;
+      if (s != EG) continue;
       if (m == 0) {   // the previous unit's last block, then that unit is complete
         float ap0 = apc0, ap1 = apc1;
         epi(ewp, acc[(MB - 1) & 1], ap0, ap1);
         apc0 = 0.f;
         apc1 = 0.f;
-        if (NAIS_X6N_ABL & 8) {
-          S += ap0 + ap1;
-        } else if constexpr (NHU == 1) {
+        if constexpr (NHU == 1) {
           tail(prev >= 0 ? prev : 0, ap0, ap1, live);
         } else {                 // an item's units add their partials; its last one, the tail
           pa0 = HPV == 0 ? ap0 : pa0 + ap0;
@@ -1758,12 +1739,6 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       } else if (MMA) {
         epi(ewc + 16 * (m - 1), acc[(m - 1) & 1], apc0, apc1);
       }
-    }
-    if (NAIS_X6N_ABL & 1) {   // keep every accumulator alive without VALU work
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) asm volatile("" ::"v"(acc[k][nb]));
     }
   };
 
@@ -1854,7 +1829,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       };
       one(std::integral_constant<int, 0>{});
       if constexpr (GU == 2) one(std::integral_constant<int, 1>{});
-      if (!(NAIS_X6N_ABL & 16)) __syncthreads();
+      __syncthreads();
     };
     for (int g = 0; g < ngroups; g += 2) {
       group(g, std::integral_constant<int, 0>{});
@@ -2594,8 +2569,8 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
       // one unit up to 64 hidden units, two at H = 128 (D = 128 with 32-hidden units, MB = 2:
       // 1 % slower in the same process, profiles/r4/ab8)
       constexpr int D = 2 * DH;
-      constexpr int MB = (D == 128 && NAIS_X6N_MB128 == 2) ? 2 : (HB <= 2 ? 2 * HB : 4);
-      constexpr int NHU = (D == 128 && NAIS_X6N_MB128 == 2) ? HB : (HB <= 2 ? 1 : 2);
+      constexpr int MB = HB <= 2 ? 2 * HB : 4;
+      constexpr int NHU = HB <= 2 ? 1 : 2;
       constexpr bool REG = VarT<VAR>::REGION;
       using CN = CfgN<D, MB, NHU>;
       const size_t lds = CN::BYTES;
