@@ -84,6 +84,13 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse N>1 on one GPU")
+    ap.add_argument("--ab", action="store_true",
+                    help="A/B runs only: read the pairs-route knobs from the environment (NAIS_PAIR_TABLE_CUS, "
+                         "NAIS_PAIR_CU_LAYOUT, NAIS_PAIR_BLOCK_COLS, NAIS_PAIR_FUSED_TOPK, NAIS_PAIR_LPT_ORDER, "
+                         "NAIS_PAIR_TABLE_GATHER_FRAC, NAIS_PAIR_FIRST_TABLE_ALL_CUS); the line records them")
+    ap.add_argument("--emulate-world", type=int, default=1,
+                    help="one process: time rank 0's column shard of an N-GPU pairs job (its tables, "
+                         "gathers and local top-k; no collective)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "pairs", "direct"],
                     help="auto: pairs for config 4 (each (item, candidate) pair shared by ~50 users), "
                          "direct for config 5's 4096-user subset (sharing ~1)")
@@ -399,17 +406,25 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
         keep = keep.view(b, n, H).cpu().numpy()
         h, d, l = host[0]
         r = train_oracle.train_step_basic(p0, np.repeat(h[None], b, 0), d, l, keep=keep, drop_p=0.5)
-        worst, bad = 0.0, 0
+        # every element within rtol 1e-4 / atol 2e-5 of the oracle, except elements whose oracle
+        # gradient is within 1e-4 of the tensor's largest (fp32 noise may flip the sign of
+        # Adagrad's first +-lr step), and those within the 2 lr such a flip moves them
+        bad, unexplained, worst_dev = 0, 0, 0.0
         for k, v in p0.items():
-            want, _ = train_oracle.adagrad(v, np.zeros_like(v), r["grads"][k].reshape(v.shape), 0.01, 1)
+            g = r["grads"][k].reshape(v.shape)
+            want, _ = train_oracle.adagrad(v, np.zeros_like(v), g, 0.01, 1)
             miss = ~np.isclose(p1[k], want, rtol=1e-4, atol=2e-5)
+            tiny = np.abs(g) <= 1e-4 * float(np.abs(g).max())
             bad += int(miss.sum())
-            worst = max(worst, float(miss.mean()))
+            unexplained += int((miss & ~tiny).sum())
+            if miss.any():
+                worst_dev = max(worst_dev, float(np.abs(p1[k] - want)[miss].max()))
         out["self_check"] = {"oracle": "oracle/train_oracle.py (float64, dropout mask injected)",
                              "loss": loss0, "oracle_loss": float(r["loss"]),
                              "loss_ok": abs(loss0 - float(r["loss"])) <= 1e-5,
-                             "params_off_rtol_1e-4": bad, "worst_fraction_off": worst,
-                             "params_ok": worst <= 1e-3,
+                             "params_off_rtol_1e-4": bad, "params_off_nontiny_grad": unexplained,
+                             "max_dev_off": worst_dev,
+                             "params_ok": unexplained == 0 and worst_dev <= 2 * 0.01,
                              "seconds": round(time.perf_counter() - t0, 1)}
     del tr, opt, em, eopt, m
     torch.cuda.empty_cache()
@@ -697,22 +712,23 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
     from poi_recommendation_models_amd import catalog
     from poi_recommendation_models_amd.sharding import column_blocks, distributed_topk_pairs
-    if os.environ.get("NAIS_PAIR_TABLE_CUS"):          # A/B knobs of the table/gather overlap
-        catalog.PAIR_TABLE_CUS = int(os.environ["NAIS_PAIR_TABLE_CUS"])
-    if os.environ.get("NAIS_PAIR_CU_LAYOUT"):
-        catalog.PAIR_CU_LAYOUT = os.environ["NAIS_PAIR_CU_LAYOUT"]
-    if os.environ.get("NAIS_PAIR_BLOCK_COLS"):
-        catalog.PAIR_BLOCK_COLS = int(os.environ["NAIS_PAIR_BLOCK_COLS"])
-    for knob in ("PAIR_FUSED_TOPK", "PAIR_LPT_ORDER"):
-        if os.environ.get("NAIS_" + knob):
-            setattr(catalog, knob, os.environ["NAIS_" + knob] == "1")
-    if os.environ.get("NAIS_PAIR_TABLE_GATHER_FRAC"):
-        catalog.PAIR_TABLE_GATHER_FRAC = float(os.environ["NAIS_PAIR_TABLE_GATHER_FRAC"])
-    if os.environ.get("NAIS_PAIR_FIRST_TABLE_ALL_CUS"):
-        catalog.PAIR_FIRST_TABLE_ALL_CUS = os.environ["NAIS_PAIR_FIRST_TABLE_ALL_CUS"] == "1"
-    # NAIS_EMULATE_WORLD=N (one process): time rank 0's column shard of an N-GPU run (its tables,
+    if a.ab:   # A/B knobs of the table/gather overlap, only when asked for (--ab)
+        if os.environ.get("NAIS_PAIR_TABLE_CUS"):
+            catalog.PAIR_TABLE_CUS = int(os.environ["NAIS_PAIR_TABLE_CUS"])
+        if os.environ.get("NAIS_PAIR_CU_LAYOUT"):
+            catalog.PAIR_CU_LAYOUT = os.environ["NAIS_PAIR_CU_LAYOUT"]
+        if os.environ.get("NAIS_PAIR_BLOCK_COLS"):
+            catalog.PAIR_BLOCK_COLS = int(os.environ["NAIS_PAIR_BLOCK_COLS"])
+        for knob in ("PAIR_FUSED_TOPK", "PAIR_LPT_ORDER"):
+            if os.environ.get("NAIS_" + knob):
+                setattr(catalog, knob, os.environ["NAIS_" + knob] == "1")
+        if os.environ.get("NAIS_PAIR_TABLE_GATHER_FRAC"):
+            catalog.PAIR_TABLE_GATHER_FRAC = float(os.environ["NAIS_PAIR_TABLE_GATHER_FRAC"])
+        if os.environ.get("NAIS_PAIR_FIRST_TABLE_ALL_CUS"):
+            catalog.PAIR_FIRST_TABLE_ALL_CUS = os.environ["NAIS_PAIR_FIRST_TABLE_ALL_CUS"] == "1"
+    # --emulate-world N (one process): time rank 0's column shard of an N-GPU run (its tables,
     # gathers and local top-k; no collective) -- per-rank cost and strong-scaling headroom on one GPU
-    emulate = int(os.environ.get("NAIS_EMULATE_WORLD", "1"))
+    emulate = a.emulate_world
     P, D, H, K = a.num_pois, a.dim, a.hidden, a.topk
     users = np.arange(a.num_users)
     group = None

@@ -268,7 +268,7 @@ PAIR_SPLIT_STEP = 8
 _masked: dict = {}
 
 
-def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None):
+def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, work_queues=True):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/, re-fitted in round 3 on the fp16x6 tables:
@@ -278,17 +278,25 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None):
     memory side saturates; the round-1 figure of 60 kept the exact-fp32 leg at 160 table CUs). Picks the split that minimises the slower of the two streams (config 4: 160 of 256
     under fp16x6, config 5: 224). With the power-law prior the table stream also builds the float64
     pr_d table (~1.4e-11 s per pair on the whole chip, profiles/r2/legs_s4) and the gather stream
-    reads it too (8 more bytes per history entry and column)."""
+    reads it too (8 more bytes per history entry and column).
+
+    `work_queues`: whether this job's table AND gather launches take the work counter (the x6n
+    table kernel of the NAIS modules and the fused top-k gather). Only then may the
+    split step finer than one CU per shader engine: a fixed-grid launch on a CU count off a
+    multiple of 32 leaves an engine short and runs at the next lower multiple."""
     H, din = model.attn_layer1.weight.shape
     prec = getattr(model, "precision", "fp16x6")
     products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
+    dist = getattr(model, "VARIANT", 0) in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE)
+    D = din - 2 if dist else din
     gbytes = entries * NC * 8.0
     if prior:
         gbytes *= 2
     xcd = max(1, ncu // 8)
     # with work-queue launches the split may step finer than a CU per shader engine (x6n tables
     # and the fused gather; other table kernels keep the engine-sized steps)
-    x6n = (PAIR_WORK_QUEUE and products == 6 and din in (32, 64, 128) and not prior)
+    x6n = (PAIR_WORK_QUEUE and work_queues and products == 6 and D in (32, 64, 128) and H <= 128
+           and not prior)
     step = min(PAIR_SPLIT_STEP, xcd) if x6n else xcd
     rate = 1.5e15 if x6n else 1.25e15   # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard)
     t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else rate)
@@ -448,6 +456,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             return None
         h = int(stream_ or 0)
         if h not in wq_of:
+            if len(wq_of) >= wq_slots.numel():   # one counter per stream
+                raise RuntimeError("pairs route: more streams than work-queue counters")
             wq_of[h] = wq_slots.data_ptr() + 4 * len(wq_of)
         return wq_of[h]
 
@@ -519,7 +529,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             ld = (W + 3) // 4 * 4
             blocks = list(range(c0_all, c1_all, W))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None, J * ld * 8)
+            # both streams run as work queues only with the NAIS modules' own table kernel and
+            # the fused gather (the score-row gather and nais_dot_pair_table keep fixed grids)
+            wq_both = fused and type(model)._pair_table is _NAISDevice._pair_table
+            table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None, J * ld * 8,
+                                        work_queues=wq_both)
                          if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS)
             wq_on[0] = table_cus % max(1, ncu // 8) != 0
             if events is not None:
@@ -646,8 +660,14 @@ def usable_device_bytes(dev):
     this, so it does not depend on how much of an earlier call's memory the allocator still caches
     (mem_get_info alone counts that as used: the prior route's 60 GB of score + G rows at config 4
     then fit one pass on a fresh process and needed two after a first job)."""
+    # only cached segments with nothing allocated in them can serve a new large allocation (the
+    # allocator releases them and retries when a request finds no block); the free pieces of partly
+    # used segments ("inactive split" bytes) cannot, so they are not counted (ADVICE r4)
     free = torch.cuda.mem_get_info(dev)[0]
-    return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
+    st = torch.cuda.memory_stats(dev)
+    split = int(st.get("inactive_split_bytes.all.current", 0))
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev) - split
+    return int(free + max(0, cached))
 
 
 def _prior_entries_finite(a, b):

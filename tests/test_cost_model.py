@@ -40,3 +40,21 @@ def test_split_in_shader_engine_steps(ncu):
             if prec == "fp16x6" and not prior and catalog.PAIR_WORK_QUEUE:
                 step = min(catalog.PAIR_SPLIT_STEP, step)
             assert n % step == 0 and ncu // 4 <= n <= ncu - step
+
+
+def test_fixed_grid_routes_keep_engine_steps():
+    """a job whose gather or table launch keeps a fixed grid (the score-row gather for
+    k > 256 or rows_only, transform_attn's nais_dot_pair_table) must not get an 8-CU split step."""
+    n = auto_table_cus(_model(64, 64, "fp16x6"), 100_000, 100_000, 5_030_351, 256, False,
+                       work_queues=False)
+    assert n % 32 == 0, n
+    assert n == 160          # the classic engine-sized optimum at config 4
+
+
+def test_distance_variants_take_the_x6n_steps():
+    """din = D + 2 for the distance variants: the split model keys on D."""
+    m = _model(66, 64, "fp16x6")
+    m.VARIANT = 2            # NAIS_VARIANT_REGION_DISTANCE
+    assert auto_table_cus(m, 100_000, 100_000, 5_030_351, 256, False) % 8 == 0
+    m.VARIANT = 0
+    assert auto_table_cus(m, 100_000, 100_000, 5_030_351, 256, False) % 32 == 0

@@ -137,6 +137,53 @@ def test_config4_bench_job_vs_reference_restatement(config4_job):
     _stats("config 4 vs restatement", before)
 
 
+def test_config4_bench_job_sampled_oracle_2048_users(config4_job):
+    """2,048 of the bench job's users spread over h (every h from 1 to 200
+    several times), each against the CPU restatement on a sampled candidate set -- its top-50
+    winners plus 500 random candidates -- as config 5 does below:
+      * the winners' restated scores within SCORE_ATOL of the job's top-50 scores;
+      * no sampled non-winner beats the weakest winner in the restatement by more than the
+        4-ulp tie allowance (the selection is right on the sample);
+      * the pairs route's full score rows of these users (nais_pair_gather) within SCORE_ATOL of
+        the restatement on every sampled candidate.
+    The restatement is oracle/torch_cpu.py (the reference's ops in torch CPU, pinned to its outputs
+    by tests/test_torch_cpu_baseline.py); every 64th user also through the numpy oracle."""
+    from oracle import torch_cpu
+    from poi_recommendation_models_amd.catalog import score_catalog
+    data, p, m, csr, ids_p, sc_p = config4_job
+    P, K = data.num_pois, 50
+    h = data.hist_len()
+    users = _config4_oracle_users(h, 2048)
+    assert len(users) >= 2000 and h[users[0]] == h.min() and h[users[-1]] == h.max()
+    tm = torch_cpu.TorchNAIS(p)
+    rng = np.random.default_rng(4)
+    worst_w = worst_s = 0.0
+    for b0 in range(0, len(users), 512):
+        ub = users[b0:b0 + 512]
+        full = score_catalog(m, csr, ub, strategy="pairs").cpu().numpy()
+        for i, u in enumerate(ub):
+            hist = data.history(u)
+            cand = nais_oracle.complement_candidates(hist, P)
+            extra = rng.choice(cand, 500, replace=False)
+            probe = np.concatenate([ids_p[u].astype(np.int64), extra[~np.isin(extra, ids_p[u])]])
+            with torch.no_grad():
+                ref = tm(torch.as_tensor(hist).expand(len(probe), len(hist)),
+                         torch.as_tensor(probe)).numpy()
+            if (b0 + i) % 64 == 0:
+                oref, _ = nais_oracle.forward_basic(p, np.broadcast_to(hist, (len(probe), len(hist))), probe)
+                assert np.max(np.abs(oref - ref)) <= 1e-6, u
+            dw = float(np.max(np.abs(ref[:K] - sc_p[u])))
+            assert dw <= SCORE_ATOL, (u, dw)
+            weakest = float(ref[:K].min())
+            over = ref[K:] - weakest
+            assert np.all(over <= TIE_ULPS * np.spacing(np.float32(weakest))), (u, float(over.max()))
+            ds = float(np.max(np.abs(full[i][probe] - ref)))
+            assert ds <= SCORE_ATOL, (u, ds)
+            worst_w, worst_s = max(worst_w, dw), max(worst_s, ds)
+    print(f"config 4: {len(users)} users (h = {h[users[0]]} .. {h[users[-1]]}) on sampled candidates "
+          f"vs the restatement: max |winner score diff| {worst_w:.3g}, max |row score diff| {worst_s:.3g}")
+
+
 def test_config2_slice_both_routes():
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
     from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins

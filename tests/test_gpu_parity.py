@@ -449,9 +449,22 @@ def test_new4_validation_golden(tag, precision):
 
     class Args:
         topk = 50
+    ks = [5, 10, 15, 20, 25, 30]
     got = V.new4_validation(m, Args(), U, positives_from(z, "test"), positives_from(z, "val"), X,
-                            z["region_of"], [5, 10, 15, 20, 25, 30], z["near"])
-    np.testing.assert_allclose(np.array(got), z[f"{tag}/metrics"], atol=2.0 / U)
+                            z["region_of"], ks, z["near"])
+    # the 6-tuple exactly, not within 2/U. The "init" fixture (the reference's
+    # N(0, 0.01) init: scores bunched at 0.5) holds tie runs straddling some k; those (user, k)
+    # alone use our list, and they are exactly the fixture's own straddling pairs
+    from _helpers import assert_metrics_exact, straddles
+    rec = V.recommend(m, Args(), U, X)
+    excused = assert_metrics_exact(got, z[f"{tag}/topk_ids"], z[f"{tag}/topk_scores"], rec,
+                                   positives_from(z, "val"), positives_from(z, "test"), ks,
+                                   tie_ulps=TIE_ULPS)
+    print(f"new4/{tag}/{precision}: (user, k) excused by a straddling tie run: {excused}")
+    sc_ref = z[f"{tag}/topk_scores"]
+    assert excused == [(u, k) for k in ks for u in range(U) if straddles(sc_ref[u], k, TIE_ULPS)]
+    if not excused:
+        np.testing.assert_array_equal(np.array(got), z[f"{tag}/metrics"])
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog, score_topk
     csr = DeviceCSR.from_arrays(z["indptr"], z["indices"], P, torch.device(DEV))
     full = score_catalog(m, csr, range(U)).cpu().numpy()
