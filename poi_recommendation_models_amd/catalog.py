@@ -114,7 +114,7 @@ def score_catalog(model, train_matrix, users, region_of=None, coords=None, latlo
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
     out = torch.empty(len(users), P, dtype=torch.float32, device=dev)
     nan = torch.zeros(1, dtype=torch.int32, device=dev)
-    rc = _capi.load().nais_score_catalog(model.nais_params(), csr.indptr.data_ptr(),
+    rc = _capi.load().nais_score_catalog(model._score_params(), csr.indptr.data_ptr(),
                                          csr.indices.data_ptr(), u_dev.data_ptr(), len(users),
                                          _capi.ptr(reg), _capi.ptr(cor), _capi.ptr(llm),
                                          out.data_ptr(), P, nan.data_ptr(), _capi.stream_handle(dev))
@@ -193,7 +193,7 @@ def score_topk(model, train_matrix, users, k, region_of=None, coords=None, latlo
     sc = torch.empty(n, k, dtype=torch.float32, device=dev)
     counters = torch.zeros(2, dtype=torch.int32, device=dev)
     lib = _capi.load()
-    prm = model.nais_params()
+    prm = model._score_params()
     pri, pri_coords = None, None
     if prior is not None:
         pa, pb, alpha, pc = prior
@@ -289,6 +289,7 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     products = 1 if prec == "fp32" else (6 if prec.startswith("fp16x6") else 3)
     dist = getattr(model, "VARIANT", 0) in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE)
     D = din - 2 if dist else din
+    D = next((w for w in (8, 16, 32, 64, 128) if w >= D), D)   # the padded width the kernels run
     gbytes = entries * NC * 8.0
     if prior:
         gbytes *= 2
@@ -403,7 +404,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     up_dev = torch.from_numpy(up.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
     u_all = up_dev[:n]
     reg, cor, llm = _side_inputs(model, dev, region_of, coords, latlon_mat)
-    prm = model.nais_params()
+    prm = model._score_params()
     rowmap = torch.empty(P, dtype=torch.int32, device=dev)
     items = torch.empty(P, dtype=torch.int64, device=dev)
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)

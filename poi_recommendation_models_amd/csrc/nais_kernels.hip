@@ -1402,9 +1402,10 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 }
 
 // ---------------------------------------------------------------------------------------------
-// The fp16x6 item-side kernel on v_mfma_f32_16x16x32_f16 ("x6n", D in {32, 64}, H <= 64, NAIS_basic
-// and the region variant): the x3b factorisation A_j t_c, the same six products of exact hi / mid /
-// lo f16 pieces, the same per-wave candidate scale and pipelined epilogue, in 16 x 16 output tiles:
+// The fp16x6 item-side kernel on v_mfma_f32_16x16x32_f16 ("x6n", D in {32, 64, 128}, H <= 128 in
+// hidden-unit slices, every variant: basic, region, region_distance, distance): the x3b
+// factorisation A_j t_c, the same six products of exact hi / mid / lo f16 pieces, the same per-wave
+// candidate scale and pipelined epilogue, in 16 x 16 output tiles:
 //   A (16 hidden x 32 dims)    lane l: hidden 16 m + (l & 15), dims 32 s + 8 (l >> 4) .. + 8 (LDS ring)
 //   B (32 dims x 16 cands)     lane l: candidate 16 nb + (l & 15), the same dims (VGPRs, 2 blocks nb)
 //   C (16 hidden x 16 cands)   lane l: candidate (l & 15), hidden 16 m + 4 (l >> 4) + r
@@ -1415,12 +1416,20 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // of 8 of 32). The attention logit of a candidate is summed over the four lane groups by one
 // v_permlane32_swap + one v_permlane16_swap for both candidate blocks at once; s = h_j . t_c comes
 // from a per-chunk s tile (items x candidates) that each wave parks in its own LDS slot in
-// [candidate][item] order, one ds_read per pair.
+// [candidate][item] order, one ds_read per pair. The distance variants' two extra inputs
+// sigmoid(dist_layer(scale * |dlat, dlng|)) (model.py:265-267, 369-371) are one exact fp32
+// v_mfma_f32_16x16x4_f32 K-step per (hidden block, candidate block): A = the two W1 columns of the
+// block's hidden units (K rows 2, 3 zero), B = the pair's two features scaled by S (K rows 2, 3
+// zero). Each lane computes ONE feature of one pair -- lane group g: feature g & 1 of candidate
+// block g >> 1 -- and one v_permlane32_swap hands groups 0 / 1 both blocks' features.
 // ---------------------------------------------------------------------------------------------
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ floatx4 mfma16n(half8 a, half8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx4 mfma16f32(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 // the six fp16x6 products, smallest terms first (as mfma_pieces<3>)
 __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const half8 (&b)[3], floatx4 c) {
@@ -1444,7 +1453,7 @@ struct X6Slices {
   static constexpr int cur = C, prev = P, built = B;
 };
 
-template <int D, int MB, int NHU>
+template <int D, int MB, int NHU, bool DIST = false>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
   static constexpr int NE = MB * KS * 64;              // uint4 entries per unit and piece
@@ -1457,19 +1466,24 @@ struct CfgN {
   static constexpr int HP = HPU * NHU;                 // hidden units, padded
   static constexpr int EPI = 2 * HP;                   // [b1 | w2] by hidden unit
   static constexpr int SVP = JCB + 1;                  // s image pitch (floats): [cand][item]
+  static constexpr int ADN = DIST ? HP * 4 : 0;        // distance columns of W1: [hidden][4] (2, 3 zero)
   static constexpr size_t BYTES = size_t(2) * GU * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
-                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4;
+                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4 +
+                                  size_t(ADN) * 4 + (DIST ? size_t(JCB) * 16 : 0);
   static_assert(BYTES <= 160 * 1024, "x6n: LDS");
   static_assert((2 * GU) % NHU == 0, "x6n: a group pair spans whole items");
 };
 
-template <int D, int MB, int NHU, bool REGION>
+template <int D, int MB, int NHU, int VAR>
 __global__ void __launch_bounds__(512, 1)
 catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
                          const int64_t* __restrict__ indices, const int32_t* __restrict__ users,
-                         const int64_t* __restrict__ region_of, float* __restrict__ scores,
+                         const int64_t* __restrict__ region_of, const double* __restrict__ coords,
+                         const double* __restrict__ latlon_mat, float* __restrict__ scores,
                          int64_t score_ld, int32_t* __restrict__ nan_count, TableOut tab) {
-  using C = CfgN<D, MB, NHU>;
+  constexpr bool REGION = VarT<VAR>::REGION;
+  constexpr bool DIST = VarT<VAR>::DIST;
+  using C = CfgN<D, MB, NHU, DIST>;
   constexpr int KS = C::KS, NE = C::NE, GU = C::GU, JCB = C::JCB, EPT = C::EPT, HP = C::HP;
   constexpr int HPU = C::HPU, EPI = C::EPI, NW = C::NW, THREADS = C::THREADS, CPB = C::CPB;
   constexpr int SVP = C::SVP;
@@ -1482,6 +1496,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* hrows = red + 16;                                         // [JCB][D]
   int32_t* hid = reinterpret_cast<int32_t*>(hrows + JCB * D);
   float* svt = reinterpret_cast<float*>(hid + JCB);                // per wave [32 cands][SVP]
+  float* Adn = svt + NW * 32 * SVP;                                // DIST: W1 distance columns [HP][4]
+  double* hco = reinterpret_cast<double*>(Adn + C::ADN);           // DIST: the chunk's coordinates [JCB][2]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = lane >> 4, l16 = lane & 15;
   const int64_t clim = tab.e ? std::min<int64_t>(p.P, tab.col0 + tab.cols) : p.P;
@@ -1506,7 +1522,15 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const int i = f % HP;
     Eimg[f] = (i < p.H) ? (f < HP ? p.b1[i] : p.w2[i]) : 0.f;
   }
-  const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg
+  if constexpr (DIST) {
+    for (int f = tid; f < C::ADN; f += THREADS) {
+      const int i = f >> 2, k = f & 3;
+      Adn[f] = (i < p.H && k < 2) ? p.w1[(int64_t)i * p.din + D + k] : 0.f;
+    }
+  }
+  const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg / Adn
+  // DIST: this lane's feature row of dist_layer (feature grp & 1, model.py:265 / 369)
+  const DistW dw = DIST ? load_distw<VAR>(p, grp & 1) : DistW{0.f, 0.f, 0.f, 0.f};
 
   float SAcur = 1.f;   // the W1 registers' current scale (rescaled per chunk)
 
@@ -1521,6 +1545,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float St = 1.f;
   int64_t cbase = 0, cout = 0;
   bool vout = false;
+  double fclat = 0.0, fclon = 0.0;     // DIST: coordinates of this lane's feature candidate
+  const double* llrow = nullptr;       // DIST, latlon_mat mode: its row of the matrix
   for (int64_t it = 0;; ++it) {
   if (tab.work) {
     __syncthreads();   // the previous item's readers of wi_sh, hrows, hid and the ring are done
@@ -1549,6 +1575,16 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // L ^ 16 alike): lane groups 0 / 2 carry e, groups 1 / 3 e * s
     cout = cbase + 16 * (lane >> 5) + l16;
     vout = cout < clim;
+    if constexpr (DIST) {   // lane group g computes feature g & 1 of candidate block g >> 1
+      const int64_t fc = cbase + 16 * (grp >> 1) + l16;
+      const int64_t fcc = fc < clim ? fc : p.P - 1;
+      if (coords) {
+        fclat = coords[2 * fcc];
+        fclon = coords[2 * fcc + 1];
+      } else {
+        llrow = latlon_mat + fcc * p.P * 2;
+      }
+    }
     // ---- candidate operands: two blocks of 16, one scale S_t per wave, split into B fragments
     {
       float tmax = 0.f;
@@ -1595,6 +1631,28 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   float* sv_mine = svt + wave * 32 * SVP;
   int64_t j0 = 0;
   float pa0 = 0.f, pa1 = 0.f;                 // logit partials of the item's earlier units
+  int jn_cur = 1;                             // rows of the current chunk
+  float Sd = 1.f;                             // DIST: the accumulators' scale S = S_A * S_t
+  float fB0 = 0.f, fB1 = 0.f;                 // DIST: B operands (the item's features, blocks 0 / 1)
+  // the distance features of chunk item `item` against this lane's feature candidate, exactly as
+  // the other kernels form them (dist_feature: float64 |dlat|, |dlng| cast to float32, x scale,
+  // dist_layer row, sigmoid), scaled by S; groups 0 / 1 then hold both blocks' B operands
+  auto feats = [&](int item) __attribute__((always_inline)) {
+    item = std::min(item, jn_cur - 1);        // a stale step past the chunk (its MFMAs are unused)
+    float ll0, ll1;
+    if (coords) {
+      ll0 = (float)fabs(fclat - hco[2 * item]);
+      ll1 = (float)fabs(fclon - hco[2 * item + 1]);
+    } else {
+      const int64_t hj = hid[item];
+      ll0 = (float)llrow[2 * hj];
+      ll1 = (float)llrow[2 * hj + 1];
+    }
+    const float f = dist_feature(dw, ll0, ll1) * Sd;   // exact power-of-two scaling
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
+    fB0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
+    fB1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
+  };
 
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
   // of the block size (the D = 64 / 128 shapes) it has no branch, so the scheduler can spread it
@@ -1690,6 +1748,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     };
     half8 a_nx[3];
     if (MMA) aload(0, a_nx);
+    if constexpr (DIST && MMA && HC == 0) feats(NHU == 1 ? cur : cur / NHU);   // once per item
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int m = g / KS, s = g % KS;
@@ -1708,6 +1767,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (g + 1 < NG) aload(g + 1, a_nx);
         acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
         acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
+        if constexpr (DIST) {
+          if (s == KS - 1) {   // the block's two distance columns: one exact fp32 K-step
+            const float ad = Adn[(HPU * HC + 16 * m + l16) * 4 + grp];
+            acc[m & 1][0] = mfma16f32(ad, fB0, acc[m & 1][0]);
+            acc[m & 1][1] = mfma16f32(ad, fB1, acc[m & 1][1]);
+          }
+        }
         // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
         // against the last group; D = 64 unchanged -- profiles/r4/ab6)
         if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
@@ -1757,7 +1823,15 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       reinterpret_cast<float4*>(hrows)[f] = v;
       hmax = fmaxf(hmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
-    for (int jj = tid; jj < jn; jj += THREADS) hid[jj] = (int32_t)indices[hbeg + j0 + jj];
+    for (int jj = tid; jj < jn; jj += THREADS) {
+      const int64_t item = indices[hbeg + j0 + jj];
+      hid[jj] = (int32_t)item;
+      if (DIST && coords) {
+        hco[2 * jj] = coords[2 * item];
+        hco[2 * jj + 1] = coords[2 * item + 1];
+      }
+    }
+    jn_cur = jn;
     const float Hm = block_max_n<NW>(hmax, red);   // barrier: chunk published
     const float SA = pow2_scale(Wmax * Hm);
     const float rs = SA / SAcur;                   // exact power-of-two ratio
@@ -1769,6 +1843,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         for (int x = 0; x < 8; ++x) wv[h][q][x] *= rs;
     SAcur = SA;
     const float Sacc = SA * St, invS = 1.f / Sacc;
+    Sd = Sacc;
     for (int f = lane; f < EPI; f += 64) Escl[wave * EPI + f] = Eimg[f] * (f < HP ? Sacc : invS);
     {   // s tile of the chunk: items (pieces of h * S_h, M) x this wave's candidates (N), kept as
         // s = value / (S_h S_t) in the wave's own LDS slot, [candidate][item]
@@ -2545,61 +2620,48 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
   }
 }
 
-// the 16x16x32 item-side kernel instead of x3b for the fp16x6 shapes it covers (default since round
-// 4: standalone config-4 table block 2.179 -> 1.990 ms, the job 623 -> 601 ms, profiles/r4/x6n;
-// A/B: NAIS_X6N=0 / 1 in the environment, read once per process)
-#ifndef NAIS_X6N_DEFAULT
-#define NAIS_X6N_DEFAULT 1
-#endif
-bool x6n_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("NAIS_X6N");
-    return e && e[0] ? e[0] == '1' : NAIS_X6N_DEFAULT != 0;
-  }();
-  return on;
-}
-
+// the 16x16x32 item-side kernel (x6n) instead of x3b / the per-pair split kernel for every fp16x6
+// shape it covers: D in {32, 64, 128}, H <= 128, every variant (the distance variants since round 5).
+// Round-4 A/B against x3b at config 4: standalone 512-column table block 2.179 -> 1.990 ms, the job
+// 623 -> 601 ms (profiles/r4/x6n); at D = H = 128 against the per-pair split kernel: config-5 direct
+// 6.35e7 -> 7.32e7 pairs/s (profiles/r4/d128). The A/B switch is gone; x3b keeps fp16x3.
 template <int DH, int HB, int VAR, int NPC = 2>
 int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t* indices,
                        const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                        const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
                        hipStream_t stream, const TableOut& tab = TableOut{}) {
-  if constexpr (NPC == 3 && !VarT<VAR>::DIST && (DH == 16 || DH == 32 || DH == 64)) {
-    if (x6n_enabled()) {
-      // one unit up to 64 hidden units, two at H = 128 (D = 128 with 32-hidden units, MB = 2:
-      // 1 % slower in the same process, profiles/r4/ab8)
-      constexpr int D = 2 * DH;
-      constexpr int MB = HB <= 2 ? 2 * HB : 4;
-      constexpr int NHU = HB <= 2 ? 1 : 2;
-      constexpr bool REG = VarT<VAR>::REGION;
-      using CN = CfgN<D, MB, NHU>;
-      const size_t lds = CN::BYTES;
-      auto kern = catalog_score_x6n_kernel<D, MB, NHU, REG>;
-      static bool attr_set = false;
-      if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-      }
-      dim3 grid = tab.e ? table_grid(tab, nb, CN::CPB) : cat_grid(d.P, nb, CN::CPB);
-      TableOut t = tab;
-      if (t.e && t.work) {   // work queue: one workgroup per CU of the stream's mask (the LDS
-        t.ngroups = (int32_t)grid.y;   // holds one), items tile-major
-        t.ntiles = (int32_t)grid.x;
-        const int ncu = nais_internal_stream_cus(stream);
-        if (ncu <= 0) return fail(NAIS_E_HIP, "device attributes");
-        grid = dim3((unsigned)std::min<int64_t>((int64_t)grid.x * grid.y, ncu), 1, 1);
-        if (hipMemsetAsync(t.work, 0, sizeof(int32_t), stream) != hipSuccess)
-          return fail(NAIS_E_HIP, "hipMemsetAsync(work)");
-      } else {
-        t.work = nullptr;
-      }
-      hipLaunchKernelGGL(kern, grid, dim3(CN::THREADS), lds, stream, d, indptr, indices, users,
-                         region_of, scores, ld, nan_count, t);
-      return check_launch("catalog_score_x6n_kernel");
+  if constexpr (NPC == 3 && (DH == 16 || DH == 32 || DH == 64)) {
+    // one unit up to 64 hidden units, two at H = 128 (D = 128 with 32-hidden units, MB = 2:
+    // 1 % slower in the same process, profiles/r4/ab8)
+    constexpr int D = 2 * DH;
+    constexpr int MB = HB <= 2 ? 2 * HB : 4;
+    constexpr int NHU = HB <= 2 ? 1 : 2;
+    using CN = CfgN<D, MB, NHU, VarT<VAR>::DIST>;
+    const size_t lds = CN::BYTES;
+    auto kern = catalog_score_x6n_kernel<D, MB, NHU, VAR>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
     }
-  }
-  if constexpr (DH % 8 != 0) {
+    dim3 grid = tab.e ? table_grid(tab, nb, CN::CPB) : cat_grid(d.P, nb, CN::CPB);
+    TableOut t = tab;
+    if (t.e && t.work) {   // work queue: one workgroup per CU of the stream's mask (the LDS
+      t.ngroups = (int32_t)grid.y;   // holds one), items tile-major
+      t.ntiles = (int32_t)grid.x;
+      const int ncu = nais_internal_stream_cus(stream);
+      if (ncu <= 0) return fail(NAIS_E_HIP, "device attributes");
+      grid = dim3((unsigned)std::min<int64_t>((int64_t)grid.x * grid.y, ncu), 1, 1);
+      if (hipMemsetAsync(t.work, 0, sizeof(int32_t), stream) != hipSuccess)
+        return fail(NAIS_E_HIP, "hipMemsetAsync(work)");
+    } else {
+      t.work = nullptr;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(CN::THREADS), lds, stream, d, indptr, indices, users,
+                       region_of, coords, latlon_mat, scores, ld, nan_count, t);
+    return check_launch("catalog_score_x6n_kernel");
+  } else if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
   } else if constexpr ((VarT<VAR>::DIST && !CfgB<DH, HB, true, WAVES, NPC>::PIPE) ||

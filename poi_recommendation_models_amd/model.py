@@ -55,6 +55,10 @@ class BCELoss(nn.BCELoss):
         return super().forward(input, target)
 
 
+# embedding widths the scoring kernels are compiled for (MFMA K tiles); others are zero-padded
+NATIVE_WIDTHS = (8, 16, 32, 64, 128)
+
+
 class _NAISDevice(nn.Module):
     """Shared plumbing: parameter struct for the C-ABI, device checks, NaN reporting."""
 
@@ -130,6 +134,63 @@ class _NAISDevice(nn.Module):
             p.dist_b = self.dist_layer.bias.data_ptr()
         return p
 
+    def _score_params(self) -> _capi.NaisParams:
+        """`nais_params_t` for the scoring / forward kernels. Those are compiled for the embedding
+        widths D in NATIVE_WIDTHS (the MFMA K tiles); any other D <= 128 (the reference builds
+        Linear(embed_size, hidden_size) for any size, model.py:9-38) is served from zero-padded
+        copies: the tables padded to the next native width (each half separately for the region
+        variants' [E | region] rows), attn_layer1's columns placed at the padded positions, the
+        distance columns after them. Exact: a padded dimension contributes 0 * x = 0 to W1 x and
+        to h . t, and the per-wave power-of-two scales see the same maxima. The copies are rebuilt
+        when a parameter changes (tensor version counter). Training reads the parameters as they
+        are (the training kernels take any D, H <= 128)."""
+        D = int(self.embed_size)
+        if D in NATIVE_WIDTHS:
+            return self.nais_params()
+        Dp = next((w for w in NATIVE_WIDTHS if w >= D), None)
+        if Dp is None:
+            raise RuntimeError(f"embed_size {D} > 128: the scoring kernels hold a 128-wide embedding "
+                               "tile at most (LDS / VGPR budget)")
+        region = self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE)
+        dist = self.VARIANT in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE)
+        eh, et = self._item_tables()
+        er = self.embed_region.weight if region else None
+        w1 = self.attn_layer1.weight
+        srcs = [t for t in (eh, et, er, w1) if t is not None]
+        key = tuple((t.data_ptr(), t._version) for t in srcs)
+        cache = self.__dict__.get("_pad_cache")
+        if cache is None or cache[0] != key:
+            with torch.no_grad():
+                H = w1.shape[0]
+                w1p = torch.zeros(H, Dp + (2 if dist else 0), dtype=w1.dtype, device=w1.device)
+                if region:
+                    if eh.shape[1] * 2 != D:
+                        raise ValueError(f"region variants need an even embed_size (got {D}): the "
+                                         "[history | region] rows are 2 * int(embed_size / 2) wide")
+                    half, hp = D // 2, Dp // 2
+                    pad = lambda t: torch.nn.functional.pad(t, (0, hp - half)).contiguous()
+                    tabs = (pad(eh), pad(et), pad(er))
+                    w1p[:, :half] = w1[:, :half]
+                    w1p[:, hp:hp + half] = w1[:, half:D]
+                else:
+                    pad = lambda t: torch.nn.functional.pad(t, (0, Dp - D)).contiguous()
+                    tabs = (pad(eh), pad(et), None)
+                    w1p[:, :D] = w1[:, :D]
+                if dist:
+                    w1p[:, Dp:Dp + 2] = w1[:, D:D + 2]
+            cache = (key, tabs, w1p)
+            self.__dict__["_pad_cache"] = cache
+        _, (ehp, etp, erp), w1p = cache
+        p = self.nais_params()
+        p.embed_dim = Dp
+        p.item_dim = ehp.shape[1]
+        p.din = w1p.shape[1]
+        p.embed_history, p.embed_target, p.w1 = ehp.data_ptr(), etp.data_ptr(), w1p.data_ptr()
+        if region:
+            p.region_dim = erp.shape[1]
+            p.embed_region = erp.data_ptr()
+        return p
+
     def _run_forward(self, history, target, history_region=None, target_region=None,
                      target_lat_long=None, sigmoid=True):
         if self.training:
@@ -169,7 +230,7 @@ class _NAISDevice(nn.Module):
         out = torch.empty(b, dtype=torch.float32, device=dev)
         nan = torch.zeros(1, dtype=torch.int32, device=dev)
         lib = _capi.load()
-        prm = self.nais_params()
+        prm = self._score_params()
         rc = lib.nais_forward(prm, _capi.ptr(history) if n > 0 else None, b, n,
                               history.stride(0) if n > 0 else 0, _capi.ptr(target),
                               _capi.ptr(history_region) if (history_region is not None and n > 0) else None,

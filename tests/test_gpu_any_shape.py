@@ -1,0 +1,123 @@
+"""Any embed_size / hidden_size at the drop-in (the reference builds
+Linear(embed_size, hidden_size) for any sizes, /root/reference/model.py:9-38, 100-229, 306-329).
+
+The scoring / forward kernels are compiled for embedding widths 8, 16, 32, 64, 128; other widths
+run from zero-padded copies (model._NAISDevice._score_params: each half of the region variants'
+[history | region] rows padded separately, attn_layer1's columns moved to the padded positions,
+the distance columns after them) -- exact, a padded dimension adds 0 * x = 0. Training takes the
+parameters as they are (its kernels are runtime-shaped up to 128). Checked against the numpy
+oracle (oracle/nais_oracle.py) at the north star's tolerance (scores within 1e-4, tie-aware
+top-50) on both catalog routes, the forward, and one training step at (100, 100)."""
+import numpy as np
+import pytest
+import torch
+
+from _helpers import SCORE_ATOL, assert_topk_equivalent
+from oracle import nais_oracle, train_oracle
+from test_gpu_parity import TIE_ULPS, _catalog_vs_oracle, _model, _t
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+SHAPES = [("basic", 12, 20), ("basic", 100, 100), ("basic", 40, 72), ("region", 12, 20),
+          ("region", 100, 100), ("region_distance", 100, 100), ("region_distance", 12, 20),
+          ("distance", 100, 100), ("distance", 12, 20)]
+
+
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
+@pytest.mark.parametrize("precision", ["fp16x6", "fp32", "fp16x3"])
+@pytest.mark.parametrize("variant,D,H", SHAPES)
+def test_catalog_any_width_vs_oracle(variant, D, H, precision, strategy):
+    _catalog_vs_oracle(variant, D, H, precision, strategy)
+
+
+@pytest.mark.parametrize("variant,D,H", SHAPES)
+def test_forward_any_width_vs_oracle(variant, D, H):
+    from poi_recommendation_models_amd.synthetic import init_nais_params
+    P, R, b, n = 700, 30, 45, 13
+    p = init_nais_params(P, D, H, seed=D + 7 * H, emb_std=0.3, variant=variant, num_regions=R,
+                         bias_std=0.1)
+    m = _model(variant, p)
+    rng = np.random.default_rng(D * H)
+    hist = rng.integers(0, P, (b, n)).astype(np.int64)
+    tgt = rng.integers(0, P, b).astype(np.int64)
+    tgt[4] = hist[4, 2]                                  # a masked term
+    hreg, treg = rng.integers(0, R, (b, n)), rng.integers(0, R, b)
+    ll = rng.uniform(0, 0.02, (b, n, 2)).astype(np.float32)
+    if variant == "basic":
+        got = m(_t(hist), _t(tgt))
+        ref = nais_oracle.attention_basic(p, hist, tgt)
+    elif variant == "region":
+        got = m(_t(hist), _t(tgt), _t(hreg), _t(treg))
+        ref = nais_oracle.attention_region(p, hist, tgt, hreg, treg)
+    elif variant == "region_distance":
+        got = m(_t(hist), _t(tgt), _t(hreg), _t(treg), _t(ll))
+        ref = nais_oracle.attention_region_distance(p, hist, tgt, hreg, treg, ll)
+    else:
+        got = m(_t(hist), _t(tgt), None, None, _t(ll))
+        ref = nais_oracle.attention_distance(p, hist, tgt, ll)
+    ref = nais_oracle._sigmoid(ref)
+    got = got.cpu().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL, np.max(np.abs(got[ok] - ref[ok]))
+
+
+def test_padded_copies_follow_parameter_updates():
+    """The padded copies are rebuilt when a parameter changes in place (an optimizer step)."""
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P, D, H = 900, 100, 36
+    data = make_checkins(3, P, 40, seed=5)
+    p = init_nais_params(P, D, H, seed=3, emb_std=0.3, bias_std=0.1)
+    m = _model("basic", p, precision="fp16x6")
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+    a = score_catalog(m, csr, range(3)).cpu().numpy()
+    with torch.no_grad():
+        m.embed_target.weight.mul_(0.5)
+        m.attn_layer1.weight[:, 7] += 0.25
+    b = score_catalog(m, csr, range(3)).cpu().numpy()
+    q = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    for u in range(3):
+        cand, ref = nais_oracle.catalog_scores_basic(q, data.history(u), P)
+        assert np.max(np.abs(b[u][cand] - ref)) <= SCORE_ATOL
+        assert np.max(np.abs(a[u][cand] - ref)) > 1e-3          # the old copies would fail
+
+
+def test_width_above_128_raises():
+    from poi_recommendation_models_amd.synthetic import init_nais_params
+    p = init_nais_params(50, 136, 16, seed=1)
+    m = _model("basic", p)
+    with pytest.raises(RuntimeError, match="128"):
+        m(_t(np.zeros((2, 3), np.int64)), _t(np.zeros(2, np.int64)))
+
+
+def test_training_step_100x100_vs_oracle():
+    """run.py:101-109 at embed_size = hidden_size = 100: forward (dropout off), BCELoss, backward
+    and one optim.Adagrad step against the float64 oracle (oracle/train_oracle.py)."""
+    from poi_recommendation_models_amd import optim
+    from test_gpu_train import _assert_grads, _batch, _params, _step
+    from test_gpu_train import _model as _train_model
+    from _helpers import assert_params_close, tiny_grad
+    P, D, H, n = 2000, 100, 100, 37
+    p = _params(P, D, H, seed=100)
+    m = _train_model(p)
+    hist, data, labels = _batch(P, n, 4, seed=9)
+    pred, loss, grads = _step(m, hist, data, labels)
+    r = train_oracle.train_step_basic(p, hist, data, labels)
+    assert np.max(np.abs(pred - r["pred"])) <= SCORE_ATOL
+    assert abs(loss - r["loss"]) <= 1e-5
+    _assert_grads(grads, r["grads"])
+    o = optim.Adagrad(m.parameters(), lr=0.01)
+    o.step()
+    for k, q in m.named_parameters():
+        g = r["grads"][k].reshape(p[k].shape)
+        want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), g, 0.01, 1)
+        assert_params_close(k, q.detach().cpu().numpy(), want, tiny_grad(g), 2 * 0.01)
+    # eval-mode scoring of the trained module runs from the padded copies of the new parameters
+    m.eval()
+    h0 = hist[0][:5]
+    got = m(_t(np.tile(h0, (6, 1))), _t(np.arange(6))).cpu().numpy()
+    q = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    ref, _ = nais_oracle.forward_basic(q, np.tile(h0, (6, 1)), np.arange(6))
+    assert np.max(np.abs(got - ref)) <= SCORE_ATOL
