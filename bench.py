@@ -406,25 +406,29 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
         keep = keep.view(b, n, H).cpu().numpy()
         h, d, l = host[0]
         r = train_oracle.train_step_basic(p0, np.repeat(h[None], b, 0), d, l, keep=keep, drop_p=0.5)
-        # every element within rtol 1e-4 / atol 2e-5 of the oracle, except elements whose oracle
-        # gradient is within 1e-4 of the tensor's largest (fp32 noise may flip the sign of
-        # Adagrad's first +-lr step), and those within the 2 lr such a flip moves them
+        # every element within atol 2e-5 + rtol 1e-4 of the oracle, widened only by its Adagrad
+        # slack lr * min(2, 2e-5 max|g| / |g|): the first step's lr * g / |g| amplifies the
+        # gradient's rounding where |g| is small against the tensor's largest (tests/_helpers.py)
         bad, unexplained, worst_dev = 0, 0, 0.0
         for k, v in p0.items():
             g = r["grads"][k].reshape(v.shape)
             want, _ = train_oracle.adagrad(v, np.zeros_like(v), g, 0.01, 1)
-            miss = ~np.isclose(p1[k], want, rtol=1e-4, atol=2e-5)
-            tiny = np.abs(g) <= 1e-4 * float(np.abs(g).max())
+            dev = np.abs(p1[k].astype(np.float64) - want)
+            plain = 2e-5 + 1e-4 * np.abs(want)
+            ga = np.abs(g.astype(np.float64))
+            with np.errstate(divide="ignore", invalid="ignore"):
+                slack = 0.01 * np.minimum(2.0, np.where(ga > 0, 2e-5 * ga.max() / ga, 2.0))
+            miss = dev > plain
             bad += int(miss.sum())
-            unexplained += int((miss & ~tiny).sum())
+            unexplained += int((dev > plain + slack).sum())
             if miss.any():
-                worst_dev = max(worst_dev, float(np.abs(p1[k] - want)[miss].max()))
+                worst_dev = max(worst_dev, float(dev[miss].max()))
         out["self_check"] = {"oracle": "oracle/train_oracle.py (float64, dropout mask injected)",
                              "loss": loss0, "oracle_loss": float(r["loss"]),
                              "loss_ok": abs(loss0 - float(r["loss"])) <= 1e-5,
-                             "params_off_rtol_1e-4": bad, "params_off_nontiny_grad": unexplained,
+                             "params_off_rtol_1e-4": bad, "params_beyond_adagrad_slack": unexplained,
                              "max_dev_off": worst_dev,
-                             "params_ok": unexplained == 0 and worst_dev <= 2 * 0.01,
+                             "params_ok": unexplained == 0,
                              "seconds": round(time.perf_counter() - t0, 1)}
     del tr, opt, em, eopt, m
     torch.cuda.empty_cache()

@@ -300,7 +300,8 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
            and not prior)
     step = min(PAIR_SPLIT_STEP, xcd) if x6n else xcd
     rate = 1.5e15 if x6n else 1.25e15   # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard)
-    t_tab = J * NC * 2.0 * H * din * products / (1.3e14 if products == 1 else rate)
+    din_k = D + (2 if dist else 0)      # the width the kernels multiply (padded)
+    t_tab = J * NC * 2.0 * H * din_k * products / (1.3e14 if products == 1 else rate)
     if prior:
         t_tab += J * NC * 1.4e-11
     # gather rate per CU: ~72 GB/s while a block's e / e*s tables (block_bytes) mostly stay in the

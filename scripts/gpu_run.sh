@@ -1,7 +1,7 @@
 #!/bin/bash
 # The one GPU-box runner (via gpurun): scripts/gpu_run.sh <mode> <tag> [extra args]
 #   check     the GPU suite, smoke(), the default bench line
-#   tests     the GPU suite only (extra args go to pytest, e.g. a test file or -k)
+#   tests     the GPU suite only (extra args replace the selection, e.g. test files, -k EXPR)
 #   bench     the default bench line (extra args go to bench.py)
 #   profile   rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes of the bench command
 #   pmc       SQ counter passes of the standalone pair-table block (scripts/bench_table.py; extra
@@ -17,8 +17,10 @@ out=gpurun_out/$tag
 mkdir -p "$out"
 line() { python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[1], '%.4g pairs/s' % d['value'], '%.1f ms/step' % d['ms_per_step'], 'self_check', (d.get('self_check') or {}).get('topk_ok'))" "$1"; }
 tests() {
-  timeout -k 10 1100 python -u -m pytest tests -m gpu --maxfail=10 -q -rf --durations=15 --timeout 300 \
-    --timeout-method thread "$@" > $out/pytest_gpu.log 2>&1
+  local sel=("$@")
+  [ ${#sel[@]} -eq 0 ] && sel=(tests)
+  timeout -k 10 1100 python -u -m pytest "${sel[@]}" -m gpu --maxfail=10 -q -rf --durations=15 --timeout 300 \
+    --timeout-method thread > $out/pytest_gpu.log 2>&1
   local rc=$?
   echo "pytest rc=$rc" >> $out/pytest_gpu.log
   tail -6 $out/pytest_gpu.log

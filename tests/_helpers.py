@@ -111,35 +111,39 @@ def straddles(ref_scores, k, tie_ulps):
     return any(a < k < b for a, b in tie_groups(np.asarray(ref_scores, np.float64), 0.0, tie_ulps))
 
 
-def assert_params_close(name, got, want, tiny, max_dev, rtol=1e-4, atol=2e-5):
+def adagrad_slack(g, lr, eps=1e-5):
+    """How far one Adagrad step (run.py:89; lr * g / sqrt(G), a +-lr step at the first update) can
+    move an element when its gradient is known to eps * max|g| of the tensor (the GPU gradients:
+    observed ~1e-6, asserted 1e-4 elsewhere): lr * min(2, 2 eps max|g| / |g|) -- negligible for
+    ordinary elements, up to a sign flip (2 lr) for gradients within rounding noise of zero. Pass
+    the gradient Adagrad sees (weight decay included); sum over steps."""
+    g = np.abs(np.asarray(g, dtype=np.float64))
+    m = float(g.max()) if g.size else 0.0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(g > 0, 2.0 * eps * m / g, 2.0)
+    return lr * np.minimum(2.0, r)
+
+
+def assert_params_close(name, got, want, slack, rtol=1e-4, atol=2e-5):
     """Training parity per element (VERDICT r4 'What's weak' 1): every element of `got` within
-    rtol / atol of `want`, except elements flagged `tiny` -- their reference gradient was within
-    fp32 rounding noise of zero at some step, so Adagrad's lr * g / sqrt(G) (a +-lr step at the first
-    update, run.py:89) may take either sign -- and even those must stay within `max_dev` (the
-    2 * lr * steps such a flip can move an element). The misses are printed with their count and
-    worst relative error. Returns the number of excused elements."""
+    atol + rtol |want| of `want`, widened only by that element's Adagrad slack (adagrad_slack:
+    the update's sensitivity to the gradient's rounding, which is large only where the gradient
+    is near zero). Elements outside the plain tolerance are counted and printed with their worst
+    deviation; none may exceed its widened bound. Returns how many needed the slack."""
     got = np.asarray(got, dtype=np.float64)
     want = np.asarray(want, dtype=np.float64)
-    miss = ~np.isclose(got, want, rtol=rtol, atol=atol)
-    if not miss.any():
-        return 0
-    tiny = np.broadcast_to(np.asarray(tiny, bool), miss.shape)
     dev = np.abs(got - want)
-    rel = dev / np.maximum(np.abs(want), 1e-30)
-    print(f"{name}: {int(miss.sum())} of {miss.size} element(s) off rtol {rtol}, max |dev| "
-          f"{float(dev[miss].max()):.3g}, max rel {float(rel[miss].max()):.3g}, "
-          f"{int((miss & ~tiny).sum())} with a non-tiny gradient")
-    assert not (miss & ~tiny).any(), (name, np.argwhere(miss & ~tiny)[:8].tolist())
-    assert float(dev[miss].max()) <= max_dev, (name, float(dev[miss].max()), max_dev)
+    plain = atol + rtol * np.abs(want)
+    allowed = plain + np.broadcast_to(np.asarray(slack, dtype=np.float64), dev.shape)
+    miss = dev > plain
+    if miss.any():
+        rel = dev / np.maximum(np.abs(want), 1e-30)
+        print(f"{name}: {int(miss.sum())} of {miss.size} element(s) off rtol {rtol} / atol {atol}, "
+              f"max |dev| {float(dev[miss].max()):.3g}, max rel {float(rel[miss].max()):.3g}, "
+              f"worst dev / allowed {float((dev / allowed)[miss].max()):.3g}")
+    bad = dev > allowed
+    assert not bad.any(), (name, np.argwhere(bad)[:8].tolist(), float(dev[bad].max()))
     return int(miss.sum())
-
-
-def tiny_grad(g, rel=1e-4):
-    """Elements whose gradient is within `rel` of the tensor's largest (fp32 noise can flip their
-    sign; the GPU gradients are checked to 1e-4 x max|g| elsewhere)."""
-    g = np.asarray(g, dtype=np.float64)
-    m = float(np.abs(g).max()) if g.size else 0.0
-    return np.abs(g) <= rel * m
 
 
 def assert_metrics_exact(got, ref_ids, ref_scores, our_rec, val_pos, test_pos, k_list, tie_ulps=4):
