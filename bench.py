@@ -407,8 +407,9 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
         h, d, l = host[0]
         r = train_oracle.train_step_basic(p0, np.repeat(h[None], b, 0), d, l, keep=keep, drop_p=0.5)
         # every element within atol 2e-5 + rtol 1e-4 of the oracle, widened only by its Adagrad
-        # slack lr * min(2, 2e-5 max|g| / |g|): the first step's lr * g / |g| amplifies the
-        # gradient's rounding where |g| is small against the tensor's largest (tests/_helpers.py)
+        # slack lr * min(2, 2e-4 max|g| / |g|): the first step's lr * g / |g| amplifies the
+        # gradient's rounding (tolerance 1e-4 max|g|) where |g| is small against the tensor's
+        # largest (tests/_helpers.py::adagrad_slack)
         bad, unexplained, worst_dev = 0, 0, 0.0
         for k, v in p0.items():
             g = r["grads"][k].reshape(v.shape)
@@ -417,7 +418,7 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
             plain = 2e-5 + 1e-4 * np.abs(want)
             ga = np.abs(g.astype(np.float64))
             with np.errstate(divide="ignore", invalid="ignore"):
-                slack = 0.01 * np.minimum(2.0, np.where(ga > 0, 2e-5 * ga.max() / ga, 2.0))
+                slack = 0.01 * np.minimum(2.0, np.where(ga > 0, 2e-4 * ga.max() / ga, 2.0))
             miss = dev > plain
             bad += int(miss.sum())
             unexplained += int((dev > plain + slack).sum())
@@ -435,14 +436,19 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
     return out
 
 
-def table_kernel_name(precision, D, H):
-    """The catalog kernel nais_pair_table runs for this shape (nais_kernels.hip's dispatch)."""
-    if precision == "fp32":
+def table_kernel_name(precision, D, H, variant="basic"):
+    """The catalog kernel nais_pair_table runs for this shape (nais_kernels.hip's dispatch:
+    launch_catalog_x3b / launch_catalog_x3 / launch_catalog)."""
+    dist = variant in ("region_distance", "distance")
+    if precision == "fp32" or D < 16:
         return "catalog_score_kernel"
-    if precision.startswith("fp16x6") and D in (32, 64, 128) and H <= 128 and os.environ.get("NAIS_X6N", "1") != "0":
-        return "catalog_score_x6n_kernel (16x16x32 f16 MFMA)"
-    if D > 64 or H > 64:
-        return "catalog_score_x3_kernel" if precision.startswith("fp16x6") else "catalog_score_x3b_kernel"
+    if precision == "fp16x6" and D in (32, 64, 128) and H <= 128:
+        return ("catalog_score_x6n_kernel (16x16x32 f16 MFMA%s)"
+                % (" + a 16x16x4 f32 K-step for the distance features" if dist else ""))
+    if "pairsplit" in precision or (dist and (D > 64 or H > 64)):
+        return "catalog_score_x3_kernel"
+    if precision == "fp16x6" and (D > 64 or H > 64):
+        return "catalog_score_x3_kernel"
     return "catalog_score_x3b_kernel"
 
 
@@ -699,19 +705,6 @@ def main():
 PRIOR_A, PRIOR_B, PRIOR_ALPHA = 0.052, -1.37, 0.2   # a typical PowerLaw fit (a, b) and run.py's alpha
 
 
-def variant_leg(name, job, steps, pairs_job, dev):
-    """One warm-up and `steps` timed whole jobs of a secondary configuration (same users / POIs)."""
-    job()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        out = job()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    return {"value": pairs_job * steps / el, "unit": "pairs/s", "steps": steps, "warmup": 1,
-            "ms_per_step": el / steps * 1e3}, out
-
-
 def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     """Whole-job steps through sharding.distributed_topk_pairs (the product path)."""
     from poi_recommendation_models_amd import catalog
@@ -825,18 +818,21 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
 
-    def kernels(per, precision):
-        """(gather roofline dict, table roofline dict) of one leg's per-step event timings."""
+    def kernels(per, precision, flop_item=None, kname=None, steps=None):
+        """(gather roofline dict, table roofline dict) of one leg's per-step event timings
+        (`flop_item`: algorithmic FLOP per (pair, history item) when not NAIS_basic's; `steps`:
+        the leg's timed steps when not a_steps[precision])."""
+        ns = steps or a_steps[precision]
         # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B
         # per entry) + score rows (4 B per user x column; the fused kernel writes only the top-k
         # merges); with PAIR_TABLE_GATHER_FRAC > 0 only the gather stream's share is timed
         gbytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
         gbytes *= per.get("gather_share", 1.0)
-        g_ms = sum(per.get("gather", [])) / a_steps[precision]
-        t_ms = sum(per.get("table", [])) / a_steps[precision]
-        n_gl = max(1, per["_launches"].get("gather", 0) // a_steps[precision])
+        g_ms = sum(per.get("gather", [])) / ns
+        t_ms = sum(per.get("table", [])) / ns
+        n_gl = max(1, per["_launches"].get("gather", 0) // ns)
         table_cus = per.get("table_cus", ncu) or ncu
-        tflops = J * NC * flop_per_pair_item
+        tflops = J * NC * (flop_item or flop_per_pair_item)
         g_ach = gbytes / (g_ms * 1e-3) / 1e9 if g_ms else None
         t_ach = tflops / (t_ms * 1e-3) / 1e12 if t_ms else None
         gcus = ncu - table_cus if table_cus < ncu else ncu
@@ -854,7 +850,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "launches_per_step": n_gl, "ms_per_step": g_ms, "cus": gcus,
         }
         table = {
-            "kernel": table_kernel_name(precision, D, H) + " in table mode (nais_pair_table)",
+            "kernel": (kname or table_kernel_name(precision, D, H)) + " in table mode (nais_pair_table)",
             "bound": "mfma", "achieved": t_ach, "peak": PEAKS[precision], "unit": "TFLOP/s",
             "frac": t_ach / PEAKS[precision] if t_ach else None,
             "frac_of_its_cus": t_ach / (PEAKS[precision] * table_cus / ncu) if t_ach else None,
@@ -862,7 +858,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                            "f16 MFMA dense 2.5 PF / %d products per algorithmic fp32 product"
                            % PRODUCTS[precision]),
             "algorithmic_flop_per_step": tflops, "ms_per_step": t_ms, "cus": table_cus,
-            "launches_per_step": per["_launches"].get("table", 0) // a_steps[precision],
+            "launches_per_step": per["_launches"].get("table", 0) // ns,
         }
         return gather, table
 
@@ -949,16 +945,28 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         rd = rd.to(dev).eval()
         rd.report_nan = False
         rd.precision = a.precision
-        legs["region_distance"], rd_out = variant_leg("region_distance", lambda: _score_topk_pairs(
-            rd, csr, users, K, data.region_of, data.place_coords, None, None, force=True),
-            a.leg_steps, pairs_job, dev)
-        if not a.no_self_check:   # one user against the numpy restatement of validation.py:69-121
-            from oracle import nais_oracle
+        def rd_job(events=None):
+            return _score_topk_pairs(rd, csr, users, K, data.region_of, data.place_coords, None, None,
+                                     force=True, events=events)
+        el_rd, per_rd = run(a.precision, 1, a.leg_steps, rd_job)
+        rd_out = last["out"]
+        # SURVEY.md 8(d) FLOP per (pair, history item) with din = D + 2 (the distance columns)
+        flop_rd = 2 * (D + 2) * H + 3 * H + 4 * D
+        g_rd, t_rd = kernels(per_rd, a.precision, flop_item=flop_rd, steps=a.leg_steps,
+                             kname=table_kernel_name(a.precision, D, H, "region_distance"))
+        t_rd["algorithmic_flop_per_pair_item"] = flop_rd
+        legs["region_distance"] = {"value": pairs_job * a.leg_steps / el_rd, "unit": "pairs/s",
+                                   "steps": a.leg_steps, "warmup": 1,
+                                   "ms_per_step": el_rd / a.leg_steps * 1e3,
+                                   "roofline": t_rd, "gather": g_rd}
+        if not a.no_self_check:   # 8 users spread over h against the torch restatement of
+            from oracle import torch_cpu   # validation.py:69-121 (pinned to the reference's lists)
+            trd = torch_cpu.TorchNAISRegionDistance(p_rd)
             legs["region_distance"]["self_check"] = self_check(
-                p_rd, data, [1], rd_out[0].cpu().numpy(), rd_out[1].cpu().numpy(), K,
-                scorer=lambda u: nais_oracle.catalog_scores_region_distance(
-                    p_rd, data.history(int(u)), P, data.region_of, data.place_coords),
-                oracle_name="oracle/nais_oracle.py (numpy, region_distance)")
+                p_rd, data, spread_users(hist_len, 8), rd_out[0].cpu().numpy(), rd_out[1].cpu().numpy(), K,
+                scorer=lambda u: torch_cpu.region_distance_scores(
+                    trd, data.history(int(u)), P, data.region_of, data.place_coords),
+                oracle_name="oracle/torch_cpu.py (region_distance)")
         legs["region_distance"]["what"] = ("NAIS_region_distance_Embedding (model.py:246-297) on the same "
                                            "users / POIs: [h | region] rows, distance features from the POI "
                                            "coordinates, %s tables" % a.precision)
