@@ -1634,9 +1634,12 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   int jn_cur = 1;                             // rows of the current chunk
   float Sd = 1.f;                             // DIST: the accumulators' scale S = S_A * S_t
   float fB0 = 0.f, fB1 = 0.f;                 // DIST: B operands (the item's features, blocks 0 / 1)
+  float fN0 = 0.f, fN1 = 0.f;                 // DIST: the next item's, computed one item ahead
   // the distance features of chunk item `item` against this lane's feature candidate, exactly as
   // the other kernels form them (dist_feature: float64 |dlat|, |dlng| cast to float32, x scale,
-  // dist_layer row, sigmoid), scaled by S; groups 0 / 1 then hold both blocks' B operands
+  // dist_layer row, sigmoid), scaled by S; groups 0 / 1 then hold both blocks' B operands. Formed
+  // one item ahead (mid-step of the item before), so its latency (LDS, exp, rcp) hides under
+  // that item's MFMAs
   auto feats = [&](int item) __attribute__((always_inline)) {
     item = std::min(item, jn_cur - 1);        // a stale step past the chunk (its MFMAs are unused)
     float ll0, ll1;
@@ -1650,8 +1653,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
     const float f = dist_feature(dw, ll0, ll1) * Sd;   // exact power-of-two scaling
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
-    fB0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
-    fB1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
+    fN0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
+    fN1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
   };
 
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
@@ -1748,7 +1751,10 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     };
     half8 a_nx[3];
     if (MMA) aload(0, a_nx);
-    if constexpr (DIST && MMA && HC == 0) feats(NHU == 1 ? cur : cur / NHU);   // once per item
+    if constexpr (DIST && MMA && HC == 0) {   // the item's features (formed one item ahead)
+      fB0 = fN0;
+      fB1 = fN1;
+    }
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int m = g / KS, s = g % KS;
@@ -1777,6 +1783,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
         // against the last group; D = 64 unchanged -- profiles/r4/ab6)
         if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
+        // the next item's distance features, in the item's last unit (compile-time)
+        if constexpr (DIST && HC == NHU - 1)
+          if (g == NG / 2) feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
       }
       if constexpr (D == 128) {
         // issue order of the group: the next group's A reads, then MFMAs with VALU between
@@ -1844,6 +1853,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     SAcur = SA;
     const float Sacc = SA * St, invS = 1.f / Sacc;
     Sd = Sacc;
+    if constexpr (DIST) feats(0);   // the chunk's first item (hco / hid published by the barrier above)
     for (int f = lane; f < EPI; f += 64) Escl[wave * EPI + f] = Eimg[f] * (f < HP ? Sacc : invS);
     {   // s tile of the chunk: items (pieces of h * S_h, M) x this wave's candidates (N), kept as
         // s = value / (S_h S_t) in the wave's own LDS slot, [candidate][item]

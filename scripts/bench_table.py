@@ -26,16 +26,26 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--lib", action="append", default=[])
     ap.add_argument("--only", default="fp16x6")
+    ap.add_argument("--variant", default="basic", choices=["basic", "region", "region_distance", "distance"])
     a = ap.parse_args()
     from poi_recommendation_models_amd import _capi
-    from poi_recommendation_models_amd.model import NAIS_basic
-    from poi_recommendation_models_amd.synthetic import init_nais_params
+    from poi_recommendation_models_amd import model as M
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
     dev = torch.device("cuda", 0)
     P, D, H, W = a.num_pois, a.dim, a.hidden, a.cols
-    p = init_nais_params(P, D, H, seed=6, emb_std=0.3, bias_std=0.1)
-    m = NAIS_basic(P, D, H, 0.5)
+    R = 1024
+    p = init_nais_params(P, D, H, seed=6, emb_std=0.3, bias_std=0.1, variant=a.variant, num_regions=R)
+    m = {"basic": lambda: M.NAIS_basic(P, D, H, 0.5),
+         "region": lambda: M.NAIS_regionEmbedding(P, D, H, 0.5, R),
+         "region_distance": lambda: M.NAIS_region_distance_Embedding(P, D, H, 0.5, R, 1),
+         "distance": lambda: M.NAIS_distance_Embedding(P, D, H, 0.5, R, 1)}[a.variant]()
     m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()}, strict=False)
     m = m.to(dev).eval()
+    side = make_checkins(2, P, 2, seed=1, num_regions=R)
+    reg = torch.as_tensor(side.region_of, dtype=torch.int64, device=dev)
+    cor = torch.as_tensor(np.ascontiguousarray(side.place_coords, dtype=np.float64), device=dev)
+    reg_p = reg.data_ptr() if a.variant in ("region", "region_distance") else None
+    cor_p = cor.data_ptr() if a.variant in ("region_distance", "distance") else None
     items = torch.arange(P, dtype=torch.int64, device=dev)
     J = P
     libs = {"lib": _capi.load()}
@@ -55,14 +65,15 @@ def main():
             e0.record(st)
             for b in range(a.blocks):
                 c0 = (b * W) % (P - W)
-                _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, W, None, None, None,
+                _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, W, reg_p, cor_p, None,
                                                 tabs[v][0].data_ptr(), tabs[v][1].data_ptr(), W,
                                                 None, st.cuda_stream), "nais_pair_table")
             e1.record(st)
             torch.cuda.synchronize(dev)
             if r > 0:
                 times[v].append(e0.elapsed_time(e1) / a.blocks)
-    flop = J * W * (2 * D * H + 3 * H + 4 * D)
+    din = D + (2 if "distance" in a.variant else 0)
+    flop = J * W * (2 * din * H + 3 * H + 4 * D)
     base = tabs[variants[0]]
     out = {}
     for v in variants:
