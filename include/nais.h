@@ -69,14 +69,19 @@ extern "C" {
 
 /*
  * Parameters of one NAIS model: device pointers to the reference's nn.Module parameters
- * (state_dict names in comments) plus their dimensions. embed_dim must be a multiple of 8.
+ * (state_dict names in comments) plus their dimensions. The scoring entry points are compiled for
+ * embed_dim in {8, 16, 32, 64, 128}; a caller with another width <= 128 zero-pads the tables (each
+ * half of the region variants' rows separately) and attn_layer1's columns to the next of those
+ * (exact; the Python drop-in does this, model._NAISDevice._score_params). hidden: 1..256 -- above
+ * 128 for precision FP16X6 at embed_dim 32, 64, 128 and for nais_forward (NAIS_E_UNSUPPORTED
+ * otherwise); the training entry points take any embed_dim and hidden up to 128.
  */
 typedef struct nais_params {
   int32_t variant;              /* NAIS_VARIANT_* */
   int32_t embed_dim;            /* D: width of h_j (.) t (embed_size in every variant)                 */
   int32_t item_dim;             /* columns of embed_history/embed_target: D (basic, distance), D/2 (region*) */
   int32_t region_dim;           /* columns of embed_region: D/2 (region*), 0 (basic, distance)         */
-  int32_t hidden;               /* H = attn_layer1.out_features (1..128)                               */
+  int32_t hidden;               /* H = attn_layer1.out_features (1..256, see above)                    */
   int32_t din;                  /* attn_layer1.in_features: D, or D+2 for region_distance / distance   */
   int64_t num_pois;             /* P = rows of embed_history / embed_target                            */
   int64_t num_regions;          /* R = rows of embed_region (0 for basic)                              */

@@ -163,57 +163,64 @@ __device__ __forceinline__ void item_step(const float4 (&t4)[DH / 4], HPtr hrow,
                                           const float4* __restrict__ Aimg,
                                           const float* __restrict__ Adist, const EpiT& epi,
                                           float distf, int lane, float& a_out, float& s_out) {
-  floatx16 acc[HB];
+  // hidden blocks in passes of at most 4 (128 hidden units): more than 4 blocks' accumulators
+  // (H > 128) would not fit the VGPRs beside t and h; x = t * h is recomputed per pass
+  constexpr int HS = HB > 4 ? 4 : HB;
+  float sd = 0.f, ap = 0.f;
+#pragma unroll 1
+  for (int h0 = 0; h0 < HB; h0 += HS) {
+    floatx16 acc[HS];
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
+    for (int hb = 0; hb < HS; ++hb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[hb][r] = epi.bias(hb * 16 + r);
-  float sd = 0.f;
-  // Software pipeline over the DH/4 k-groups: the LDS operands of group q+1 are requested before
-  // the 4*HB MFMAs of group q issue; sched_barrier keeps the compiler from hoisting every load of
-  // the item to the top (which costs ~HB*DH VGPRs and spills at D = H = 128).
-  float4 hv_n = *reinterpret_cast<const float4*>(hrow);
-  float4 a_n[HB];
+      for (int r = 0; r < 16; ++r) acc[hb][r] = epi.bias((h0 + hb) * 16 + r);
+    // Software pipeline over the DH/4 k-groups: the LDS operands of group q+1 are requested before
+    // the 4*HS MFMAs of group q issue; sched_barrier keeps the compiler from hoisting every load of
+    // the item to the top (which costs ~HS*DH VGPRs and spills at D = H = 128).
+    float4 hv_n = *reinterpret_cast<const float4*>(hrow);
+    float4 a_n[HS];
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb) a_n[hb] = Aimg[(hb * (DH / 4)) * 64 + lane];
+    for (int hb = 0; hb < HS; ++hb) a_n[hb] = Aimg[((h0 + hb) * (DH / 4)) * 64 + lane];
 #pragma unroll
-  for (int q = 0; q < DH / 4; ++q) {
-    const float4 hv = hv_n;
-    float4 a_c[HB];
+    for (int q = 0; q < DH / 4; ++q) {
+      const float4 hv = hv_n;
+      float4 a_c[HS];
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) a_c[hb] = a_n[hb];
-    if (q + 1 < DH / 4) {
-      hv_n = *reinterpret_cast<const float4*>(hrow + 4 * (q + 1));
+      for (int hb = 0; hb < HS; ++hb) a_c[hb] = a_n[hb];
+      if (q + 1 < DH / 4) {
+        hv_n = *reinterpret_cast<const float4*>(hrow + 4 * (q + 1));
 #pragma unroll
-      for (int hb = 0; hb < HB; ++hb) a_n[hb] = Aimg[(hb * (DH / 4) + q + 1) * 64 + lane];
+        for (int hb = 0; hb < HS; ++hb) a_n[hb] = Aimg[((h0 + hb) * (DH / 4) + q + 1) * 64 + lane];
+      }
+      const float x0 = t4[q].x * hv.x, x1 = t4[q].y * hv.y, x2 = t4[q].z * hv.z, x3 = t4[q].w * hv.w;
+      if (h0 == 0) {
+        sd += x0;
+        sd += x1;
+        sd += x2;
+        sd += x3;
+      }
+#pragma unroll
+      for (int hb = 0; hb < HS; ++hb) {
+        acc[hb] = mfma32(a_c[hb].x, x0, acc[hb]);
+        acc[hb] = mfma32(a_c[hb].y, x1, acc[hb]);
+        acc[hb] = mfma32(a_c[hb].z, x2, acc[hb]);
+        acc[hb] = mfma32(a_c[hb].w, x3, acc[hb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    const float x0 = t4[q].x * hv.x, x1 = t4[q].y * hv.y, x2 = t4[q].z * hv.z, x3 = t4[q].w * hv.w;
-    sd += x0;
-    sd += x1;
-    sd += x2;
-    sd += x3;
+    if (DIST) {
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      acc[hb] = mfma32(a_c[hb].x, x0, acc[hb]);
-      acc[hb] = mfma32(a_c[hb].y, x1, acc[hb]);
-      acc[hb] = mfma32(a_c[hb].z, x2, acc[hb]);
-      acc[hb] = mfma32(a_c[hb].w, x3, acc[hb]);
+      for (int hb = 0; hb < HS; ++hb) acc[hb] = mfma32(Adist[(h0 + hb) * 64 + lane], distf, acc[hb]);
     }
-    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int hb = 0; hb < HS; ++hb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = acc[hb][r];
+        const float z = (v < 0.f) ? 0.f : v;  // ReLU that keeps NaN, as torch.relu
+        ap = __builtin_fmaf(epi.w2((h0 + hb) * 16 + r), z, ap);
+      }
   }
-  if (DIST) {
-#pragma unroll
-    for (int hb = 0; hb < HB; ++hb) acc[hb] = mfma32(Adist[hb * 64 + lane], distf, acc[hb]);
-  }
-  float ap = 0.f;
-#pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v = acc[hb][r];
-      const float z = (v < 0.f) ? 0.f : v;  // ReLU that keeps NaN, as torch.relu
-      ap = __builtin_fmaf(epi.w2(hb * 16 + r), z, ap);
-    }
   a_out = ap + __shfl_xor(ap, 32);
   s_out = sd + __shfl_xor(sd, 32);
 }
@@ -1453,26 +1460,46 @@ struct X6Slices {
   static constexpr int cur = C, prev = P, built = B;
 };
 
+// The distance features are formed one item ahead, at MFMA group 1 of the item before (region_distance
+// table block, same process, start of the item's own step / group 1 / 4 / 7: D = H = 64 2.282 /
+// 2.251 / 2.289 / 2.250 ms, D = H = 128 8.002 / 7.852 / 7.966 / 7.926 ms -- profiles/r5/feats_at).
+// The distance term as 16 VALU FMAs per 16-hidden block on the accumulators' initial values
+// (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
+// vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
+constexpr int X6N_FEATS_AT = 1;
+
 template <int D, int MB, int NHU, bool DIST = false>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
   static constexpr int NE = MB * KS * 64;              // uint4 entries per unit and piece
   static constexpr int IB = NE * 16 * 3;               // LDS bytes per unit (three pieces)
   static constexpr int GU = IB <= 24576 ? 2 : 1;       // units per ring group
-  static constexpr int JCB = 32;                       // chunk rows (the s tile's items)
   static constexpr int NW = 8, THREADS = NW * 64, CPB = NW * 32;
   static constexpr int EPT = (NE + THREADS - 1) / THREADS;   // build entries per thread and unit
   static constexpr int HPU = MB * 16;                  // hidden units per unit
   static constexpr int HP = HPU * NHU;                 // hidden units, padded
   static constexpr int EPI = 2 * HP;                   // [b1 | w2] by hidden unit
+  // distance columns of W1: [hidden][4] (2, 3 zero) for the f32 MFMA K-step
+  static constexpr int ADN = DIST ? HP * 4 : 0;
+  static constexpr size_t bytes(int jcb) {
+    return size_t(2) * GU * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 + size_t(jcb) * D * 4 +
+           size_t(jcb) * 4 + size_t(NW) * 32 * (jcb + 1) * 4 + size_t(ADN) * 4 + (DIST ? size_t(jcb) * 16 : 0);
+  }
+  // chunk rows (the s tile's items): 32, or 16 where 32 does not fit the LDS (D = 128 with 256
+  // hidden units: the per-wave [S b1 | w2 / S] copies grow with H)
+  static constexpr int JCB = bytes(32) <= 160 * 1024 ? 32 : 16;
   static constexpr int SVP = JCB + 1;                  // s image pitch (floats): [cand][item]
-  static constexpr int ADN = DIST ? HP * 4 : 0;        // distance columns of W1: [hidden][4] (2, 3 zero)
-  static constexpr size_t BYTES = size_t(2) * GU * IB + size_t(EPI) * 4 + size_t(NW) * EPI * 4 + 64 +
-                                  size_t(JCB) * D * 4 + size_t(JCB) * 4 + size_t(NW) * 32 * SVP * 4 +
-                                  size_t(ADN) * 4 + (DIST ? size_t(JCB) * 16 : 0);
+  static constexpr size_t BYTES = bytes(JCB);
+  // groups per round: a round of GQ groups (GQ * GU units) spans whole items, so every step's
+  // hidden slices are compile-time; the two ring slots alternate within it
+  static constexpr int GQ = (NHU / GU) > 2 ? NHU / GU : 2;
+  // W1 read from global memory (L2) at each build instead of held in VGPRs when a thread's
+  // share of it would take more than 32 VGPRs (D = 128 with more than 128 hidden units)
+  static constexpr bool W1G = NHU * EPT * 8 > 32;
   static_assert(BYTES <= 160 * 1024, "x6n: LDS");
-  static_assert((2 * GU) % NHU == 0, "x6n: a group pair spans whole items");
+  static_assert((GQ * GU) % NHU == 0 && GQ % 2 == 0 && GQ <= 4, "x6n: a round of groups spans whole items");
 };
+
 
 template <int D, int MB, int NHU, int VAR>
 __global__ void __launch_bounds__(512, 1)
@@ -1502,8 +1529,10 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = lane >> 4, l16 = lane & 15;
   const int64_t clim = tab.e ? std::min<int64_t>(p.P, tab.col0 + tab.cols) : p.P;
 
-  // ---- this thread's W1 values for its build entries of every unit (fp32, unscaled)
-  float wv[NHU][EPT][8];
+  // ---- this thread's W1 values for its build entries of every unit (fp32, unscaled); with W1G
+  // only their maximum (the build reads them from global memory)
+  constexpr bool W1G = C::W1G;
+  float wv[W1G ? 1 : NHU][EPT][8];
   float wmax = 0.f;
 #pragma unroll
   for (int h = 0; h < NHU; ++h)
@@ -1514,8 +1543,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       const int i = HPU * h + 16 * m + (ln & 15), k0 = 32 * s + 8 * (ln >> 4);
 #pragma unroll
       for (int x = 0; x < 8; ++x) {
-        wv[h][q][x] = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
-        wmax = fmaxf(wmax, fabsf(wv[h][q][x]));
+        const float w = (e < NE && i < p.H) ? p.w1[(int64_t)i * p.din + k0 + x] : 0.f;
+        if constexpr (!W1G) wv[h][q][x] = w;
+        wmax = fmaxf(wmax, fabsf(w));
       }
     }
   for (int f = tid; f < EPI; f += THREADS) {
@@ -1672,7 +1702,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         const int k0 = 32 * s + 8 * (ln >> 4);
         const float4 h0 = *reinterpret_cast<const float4*>(hr + k0);
         const float4 h1 = *reinterpret_cast<const float4*>(hr + k0 + 4);
-        const float* w = wv[HS][q];
+        float wg[8];   // W1G: the entry's W1 values scaled by S_A (exact power of two)
+        if constexpr (W1G) {
+          const int i = HPU * HS + 16 * ((e >> 6) / KS) + (ln & 15);
+#pragma unroll
+          for (int x = 0; x < 8; ++x) wg[x] = i < p.H ? p.w1[(int64_t)i * p.din + k0 + x] * SAcur : 0.f;
+        }
+        const float* w = W1G ? wg : wv[W1G ? 0 : HS][q];
         float a[8];
         a[0] = w[0] * h0.x; a[1] = w[1] * h0.y; a[2] = w[2] * h0.z; a[3] = w[3] * h0.w;
         a[4] = w[4] * h1.x; a[5] = w[5] * h1.y; a[6] = w[6] * h1.z; a[7] = w[7] * h1.w;
@@ -1785,7 +1821,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
         // the next item's distance features, in the item's last unit (compile-time)
         if constexpr (DIST && HC == NHU - 1)
-          if (g == NG / 2) feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
+          if (g == std::min(X6N_FEATS_AT, NG - 1)) feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
       }
       if constexpr (D == 128) {
         // issue order of the group: the next group's A reads, then MFMAs with VALU between
@@ -1844,28 +1880,31 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const float Hm = block_max_n<NW>(hmax, red);   // barrier: chunk published
     const float SA = pow2_scale(Wmax * Hm);
     const float rs = SA / SAcur;                   // exact power-of-two ratio
+    if constexpr (!W1G) {
 #pragma unroll
-    for (int h = 0; h < NHU; ++h)
+      for (int h = 0; h < NHU; ++h)
 #pragma unroll
-      for (int q = 0; q < EPT; ++q)
+        for (int q = 0; q < EPT; ++q)
 #pragma unroll
-        for (int x = 0; x < 8; ++x) wv[h][q][x] *= rs;
+          for (int x = 0; x < 8; ++x) wv[h][q][x] *= rs;
+    }
     SAcur = SA;
     const float Sacc = SA * St, invS = 1.f / Sacc;
     Sd = Sacc;
-    if constexpr (DIST) feats(0);   // the chunk's first item (hco / hid published by the barrier above)
+    if constexpr (DIST) feats(0);   // the chunk's first item (hco / hid published above)
     for (int f = lane; f < EPI; f += 64) Escl[wave * EPI + f] = Eimg[f] * (f < HP ? Sacc : invS);
     {   // s tile of the chunk: items (pieces of h * S_h, M) x this wave's candidates (N), kept as
         // s = value / (S_h S_t) in the wave's own LDS slot, [candidate][item]
       const float Sh = pow2_scale(Hm);
       const float invShSt = 1.f / (Sh * St);
-      floatx4 sacc[2][2];
+      constexpr int MI = JCB / 16;   // 16-item tiles of the chunk
+      floatx4 sacc[MI][2];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb) sacc[mi][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
         const int it = 16 * mi + l16;
         const bool ok = it < jn;
 #pragma unroll
@@ -1885,7 +1924,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         }
       }
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
@@ -1898,27 +1937,32 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     if (GU == 2 && nunits > 1) build(1, std::integral_constant<int, 1 % NHU>{}, 0, 1);
     __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
     // one group: its units' steps, each building a unit of the next group (past the chunk's end a
-    // clamped copy nobody reads) and finishing the previous unit; groups go in pairs, so every
-    // step's hidden slices are compile-time. With GU = 2 and an odd unit count the last step runs
-    // on a stale slot: only its finish of the unit before it is used.
+    // clamped copy nobody reads) and finishing the previous unit; groups go in rounds of GQ (ring
+    // slot GP & 1), so every step's hidden slices are compile-time. With GU = 2 and an odd unit
+    // count the last step runs on a stale slot: only its finish of the unit before it is used.
     auto group = [&](int g, auto gpar) __attribute__((always_inline)) {
       constexpr int GP = decltype(gpar)::value;
+      constexpr int SLOT = GP & 1;
       auto one = [&](auto itc) __attribute__((always_inline)) {
         constexpr int it = decltype(itc)::value;
-        constexpr int HC = (GP * GU + it) % NHU;   // u % NHU: a group pair spans 2 GU units,
-                                                   // a multiple of NHU (static_assert above)
+        constexpr int HC = (GP * GU + it) % NHU;   // u % NHU: a round spans GQ * GU units, a
+                                                   // multiple of NHU (static_assert in CfgN)
         using SL = X6Slices<HC, (HC + NHU - 1) % NHU, (HC + GU) % NHU>;
         const int u = g * GU + it;
         const int bu = std::min(u + GU, nunits - 1);
-        step(std::true_type{}, SL{}, ring + ((GP * GU + it) * 3) * NE, u, u - 1, u > 0, bu, GP ^ 1, it);
+        step(std::true_type{}, SL{}, ring + ((SLOT * GU + it) * 3) * NE, u, u - 1, u > 0, bu, SLOT ^ 1, it);
       };
       one(std::integral_constant<int, 0>{});
       if constexpr (GU == 2) one(std::integral_constant<int, 1>{});
       __syncthreads();
     };
-    for (int g = 0; g < ngroups; g += 2) {
+    for (int g = 0; g < ngroups; g += C::GQ) {
       group(g, std::integral_constant<int, 0>{});
       if (g + 1 < ngroups) group(g + 1, std::integral_constant<int, 1>{});
+      if constexpr (C::GQ > 2) {
+        if (g + 2 < ngroups) group(g + 2, std::integral_constant<int, 2>{});
+        if (g + 3 < ngroups) group(g + 3, std::integral_constant<int, 3>{});
+      }
     }
     const int last = ngroups * GU - 1;   // the last step's unit
     if (last == nunits - 1) {            // drain: the epilogue of the chunk's last unit, no MFMAs
@@ -2527,7 +2571,7 @@ int validate(const nais_params_t* p, Shape* sh) {
   const int D = p->embed_dim;
   if (D <= 0 || D % 8 != 0 || D > 128)
     return fail(NAIS_E_UNSUPPORTED, "embed_dim must be a multiple of 8 in [8, 128]");
-  if (p->hidden <= 0 || p->hidden > 128) return fail(NAIS_E_UNSUPPORTED, "hidden must be in [1, 128]");
+  if (p->hidden <= 0 || p->hidden > 256) return fail(NAIS_E_UNSUPPORTED, "hidden must be in [1, 256]");
   if (p->variant == NAIS_VARIANT_BASIC) {
     if (p->item_dim != D || p->din != D) return fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
   } else if (p->variant == NAIS_VARIANT_DISTANCE) {
@@ -2544,8 +2588,9 @@ int validate(const nais_params_t* p, Shape* sh) {
       return fail(NAIS_E_INVALID, "region_distance needs dist_layer weight and bias");
   }
   sh->DH = D / 2;
-  int hb = (p->hidden + 31) / 32;
+  int hb = (p->hidden + 31) / 32;   // 32-hidden blocks: 1, 2, 4 or 8 (hidden > 128)
   if (hb == 3) hb = 4;
+  if (hb > 4) hb = 8;
   sh->HB = hb;
   if (sh->DH != 4 && sh->DH != 8 && sh->DH != 16 && sh->DH != 32 && sh->DH != 64)
     return fail(NAIS_E_UNSUPPORTED, "embed_dim must be one of 8, 16, 32, 64, 128");
@@ -2582,6 +2627,10 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
                    const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                    const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
                    hipStream_t stream, const TableOut& tab = TableOut{}) {
+  if constexpr (HB > 4) {
+    return fail(NAIS_E_UNSUPPORTED, "hidden > 128: the catalog kernels take it at precision fp16x6 "
+                                    "with embed_dim 32, 64 or 128");
+  } else {
   const size_t lds = catalog_lds<DH, HB, VAR>();
   auto kern = catalog_score_kernel<DH, HB, VAR>;
   static bool attr_set = false;
@@ -2594,6 +2643,7 @@ int launch_catalog(const DevParams& d, const int64_t* indptr, const int64_t* ind
   hipLaunchKernelGGL(kern, grid, dim3(THREADS), lds, stream, d, indptr, indices, users, region_of,
                      coords, latlon_mat, scores, ld, nan_count, tab);
   return check_launch("catalog_score_kernel");
+  }
 }
 
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS per workgroup on gfx950 (MI355X_MICROARCH.md)
@@ -2610,7 +2660,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
                       const int32_t* users, int nb, const int64_t* region_of, const double* coords,
                       const double* latlon_mat, float* scores, int64_t ld, int32_t* nan_count,
                       hipStream_t stream, const TableOut& tab = TableOut{}) {
-  if constexpr (DH % 8 != 0) {  // D = 8: one K=16 f16 step would be half padding; use fp32
+  if constexpr (DH % 8 != 0 || HB > 4) {  // D = 8: one K=16 f16 step would be half padding; use fp32
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
   } else {
@@ -2645,7 +2695,7 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     // 1 % slower in the same process, profiles/r4/ab8)
     constexpr int D = 2 * DH;
     constexpr int MB = HB <= 2 ? 2 * HB : 4;
-    constexpr int NHU = HB <= 2 ? 1 : 2;
+    constexpr int NHU = HB <= 2 ? 1 : HB / 2;   // 64-hidden units: 2 at H <= 128, 4 at H <= 256
     using CN = CfgN<D, MB, NHU, VarT<VAR>::DIST>;
     const size_t lds = CN::BYTES;
     auto kern = catalog_score_x6n_kernel<D, MB, NHU, VAR>;
@@ -2671,6 +2721,9 @@ int launch_catalog_x3b(const DevParams& d, const int64_t* indptr, const int64_t*
     hipLaunchKernelGGL(kern, grid, dim3(CN::THREADS), lds, stream, d, indptr, indices, users,
                        region_of, coords, latlon_mat, scores, ld, nan_count, t);
     return check_launch("catalog_score_x6n_kernel");
+  } else if constexpr (HB > 4) {
+    return fail(NAIS_E_UNSUPPORTED, "hidden > 128: the catalog kernels take it at precision fp16x6 "
+                                    "with embed_dim 32, 64 or 128");
   } else if constexpr (DH % 8 != 0) {
     return launch_catalog<DH, HB, VAR>(d, indptr, indices, users, nb, region_of, coords, latlon_mat,
                                        scores, ld, nan_count, stream, tab);
@@ -2757,7 +2810,8 @@ int launch_forward(const DevParams& d, const int64_t* hist, int64_t b, int64_t n
   switch (HB_) {                                                                  \
     case 1: rc = FN<DH, 1, V>(__VA_ARGS__); break;                                \
     case 2: rc = FN<DH, 2, V>(__VA_ARGS__); break;                                \
-    default: rc = FN<DH, 4, V>(__VA_ARGS__); break;                               \
+    case 4: rc = FN<DH, 4, V>(__VA_ARGS__); break;                                \
+    default: rc = FN<DH, 8, V>(__VA_ARGS__); break;                               \
   }
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }

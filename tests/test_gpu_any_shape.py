@@ -63,6 +63,35 @@ def test_forward_any_width_vs_oracle(variant, D, H):
     assert np.max(np.abs(got[ok] - ref[ok])) <= SCORE_ATOL, np.max(np.abs(got[ok] - ref[ok]))
 
 
+# hidden_size > 128 (up to 256): the x6n kernel in four 64-hidden units per item (fp16x6, the
+# drop-in default) and the forward kernel in hidden passes of 128
+WIDE_H = [("basic", 64, 200), ("basic", 128, 200), ("basic", 32, 256), ("region", 64, 160),
+          ("region_distance", 64, 200), ("distance", 128, 144)]
+
+
+@pytest.mark.parametrize("strategy", ["direct", "pairs"])
+@pytest.mark.parametrize("variant,D,H", WIDE_H)
+def test_catalog_hidden_above_128_vs_oracle(variant, D, H, strategy):
+    _catalog_vs_oracle(variant, D, H, "fp16x6", strategy)
+
+
+@pytest.mark.parametrize("variant,D,H", WIDE_H + [("basic", 100, 200)])
+def test_forward_hidden_above_128_vs_oracle(variant, D, H):
+    test_forward_any_width_vs_oracle(variant, D, H)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3"])
+def test_hidden_above_128_other_precisions_raise(precision):
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    P = 300
+    data = make_checkins(2, P, 10, seed=1)
+    m = _model("basic", init_nais_params(P, 64, 200, seed=2), precision=precision)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+    with pytest.raises(RuntimeError, match="hidden > 128"):
+        score_catalog(m, csr, range(2), strategy="direct")
+
+
 def test_padded_copies_follow_parameter_updates():
     """The padded copies are rebuilt when a parameter changes in place (an optimizer step)."""
     from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog
