@@ -1467,6 +1467,10 @@ struct X6Slices {
 // (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
 // vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
 constexpr int X6N_FEATS_AT = 1;
+// Tried and not kept (profiles/r5/prio_split, standalone table blocks, same process): static
+// priority 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4) 2.026 -> 2.014 ms at
+// D = H = 64, 7.474 -> 7.479 ms at D = H = 128; the D = 128 build's two entries at a quarter and
+// three quarters of the step instead of both at its middle 7.474 -> 7.509 ms.
 
 template <int D, int MB, int NHU, bool DIST = false>
 struct CfgN {

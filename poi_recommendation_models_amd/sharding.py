@@ -226,8 +226,17 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     # the exchange: one all-gather of this rank's [n, k] block per array ([world * n, k], rank
     # order = ascending POI ranges), then the merge over the world * k candidates per user
     mark = _marker(events, dev)
-    gi = all_gather_cat(ids, group).view(world, n, k)
-    gk = all_gather_cat(out[2] if prior is not None else sc, group).view(world, n, k)
+    if prior is not None:
+        gi = all_gather_cat(ids, group).view(world, n, k)
+        gk = all_gather_cat(out[2], group).view(world, n, k)
+    else:
+        # ONE all-gather of (int32 id, f32 score bits) pairs: 8 B per entry instead of 12 in two
+        # calls (POI ids < 2^31; -1 marks a short list) -- at config 4 and N = 8 each rank receives
+        # 7 x 50k x 50 x 8 B = 140 MB over the ring
+        pk = torch.stack([ids.to(torch.int32), sc.contiguous().view(torch.int32)], dim=-1)
+        g = all_gather_cat(pk, group).view(world, n, k, 2)
+        gi = g[..., 0].to(torch.int64)
+        gk = g[..., 1].contiguous().view(torch.float32)
     mark("allgather")
     res = merge_topk_f64(gi, gk, k) if prior is not None else merge_topk(gi, gk, k)
     mark("merge")
