@@ -27,44 +27,54 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build(force=False, extra=(), out=None):
-    """Compile the kernels into OUT (or `out`, e.g. an A/B variant with extra -D flags)."""
-    if out is not None:
-        force = True
+OBJDIR = os.path.join(ROOT, "build_obj")   # per-translation-unit object cache (git- and gpurun-ignored)
+
+
+def build(force=False, extra=(), out=None, extra_for=None):
+    """Compile the kernels into OUT (or `out`, e.g. an A/B variant with extra -D flags). Objects are
+    cached per (translation unit, flags) under build_obj/: a TU is recompiled only when it or a
+    header is newer than its object, so an edit to one .hip file (or an A/B -D flag that one TU
+    reads, passed through `extra_for` = {basename: flags}) recompiles that file alone."""
+    import hashlib
     OUT_ = out or OUT
     csrc = os.path.join(HERE, "csrc")
-    deps = [*SRCS, os.path.join(ROOT, "include", "nais.h"),
-            *(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".h", ".hip")))]
-    if not force and os.path.exists(OUT_) and all(os.path.getmtime(OUT_) >= os.path.getmtime(d) for d in deps):
-        return OUT_
+    headers = [os.path.join(ROOT, "include", "nais.h"),
+               *(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".h"))]
+    hdr_time = max(os.path.getmtime(h) for h in headers)
     # -fno-slp-vectorize: hipcc's SLP pass packs adjacent f32 adds/muls into v_pk_*_f32, which
     # cost more issue slots than two scalar ops beside MFMAs (cdna_hip_programming.md, price table);
     # measured +5 % on the split-fp16 catalog kernel (profiles/r1/ab_*.json).
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize",
              "-I", os.path.join(ROOT, "include"), *extra]
-    # one object per translation unit, compiled in parallel, then one link
-    objs = [OUT_ + "." + os.path.basename(s) + ".o" for s in SRCS]
-    procs = [(subprocess.Popen([hipcc(), *flags, *PER_SRC.get(os.path.basename(s), ()), "-c", "-o", o, s],
-                               stdout=subprocess.PIPE,
-                               stderr=subprocess.STDOUT, text=True), s) for s, o in zip(SRCS, objs)]
+    os.makedirs(OBJDIR, exist_ok=True)
+    objs, todo = [], []
+    for src in SRCS:
+        f = [*flags, *PER_SRC.get(os.path.basename(src), ()), *(extra_for or {}).get(os.path.basename(src), ())]
+        key = hashlib.sha1(" ".join(f).encode()).hexdigest()[:12]
+        o = os.path.join(OBJDIR, f"{os.path.basename(src)}.{key}.o")
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_time):
+            todo.append((src, o, f))
+    if not todo and os.path.exists(OUT_) and all(os.path.getmtime(OUT_) >= os.path.getmtime(o) for o in objs):
+        return OUT_
+    # the changed translation units compiled in parallel, then one link
+    procs = [(subprocess.Popen([hipcc(), *f, "-c", "-o", o + ".tmp", src], stdout=subprocess.PIPE,
+                               stderr=subprocess.STDOUT, text=True), src, o) for src, o, f in todo]
     failed = []
-    for pr, s in procs:
-        out, _ = pr.communicate()
+    for pr, src, o in procs:
+        log, _ = pr.communicate()
         if pr.returncode != 0:
-            sys.stderr.write(out)
-            failed.append(os.path.basename(s))
-    try:
-        if failed:
-            raise RuntimeError(f"hipcc failed on {failed}")
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_ + ".tmp", *objs]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            sys.stderr.write(r.stdout + r.stderr)
-            raise RuntimeError(f"hipcc link failed ({r.returncode}): {' '.join(cmd)}")
-    finally:
-        for o in objs:
-            if os.path.exists(o):
-                os.remove(o)
+            sys.stderr.write(log)
+            failed.append(os.path.basename(src))
+        else:
+            os.replace(o + ".tmp", o)
+    if failed:
+        raise RuntimeError(f"hipcc failed on {failed}")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_ + ".tmp", *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc link failed ({r.returncode}): {' '.join(cmd)}")
     os.replace(OUT_ + ".tmp", OUT_)
     return OUT_
 

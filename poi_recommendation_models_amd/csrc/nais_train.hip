@@ -912,6 +912,9 @@ __device__ __forceinline__ float uc_load(const float* p) {
   return *p;
 }
 
+// The backward's global atomics at config 3, D = H = 128 (timing-only builds without them,
+// profiles/r5/train_bwd/r5diag): dW1 0.033 ms, history-row grads 0.022 ms of the 0.427 ms.
+
 // The general backward runs one unit per workgroup (persistent = 1 keeps W1 staged across units but
 // spills at D = H = 128: the A/B knob).
 #ifndef NAIS_GM_BWD_PERSIST
@@ -1185,6 +1188,9 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   // one unit: the loop body of the persistent form (a lambda, so that the one-unit-per-workgroup
   // launch below carries no loop state -- the persistent loop spills the D = H = 128 backward)
   auto unit = [&](int64_t un) {
+    // (slice-minor units, so that the units running at the same time add their history-row grads
+    // to different rows: backward 0.428 vs 0.428 ms; dW1 atomics into 4 / 16 replicas plus a reduce:
+    // 0.43-0.44 ms -- not kept, profiles/r5/train_bwd)
     const int64_t sl = sl0 + un / nrt, c0 = (un % nrt) * GWT, c = c0 + w;
     const bool live = c < a.b;
     const int64_t j0 = sl * 32;
