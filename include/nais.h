@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 10
+#define NAIS_ABI_VERSION 11   /* 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */

@@ -35,7 +35,7 @@ with open(os.path.join(dst, "pmc_by_kernel.csv"), "w", newline="") as fh:
 out = {}
 # the headline table kernel: basic variant, D = H = 64, fp16x6 -- the fp32 / fp16x3 /
 # region_distance legs' table launches are other instantiations and stay out of the mean
-TABLE = {"fp16x6": "catalog_score_x6n_kernel<64, 4, 1, false>",   # round 4: the 16x16x32 form
+TABLE = {"fp16x6": "catalog_score_x6n_kernel<64, 4, 1, 0>",   # the 16x16x32 form (VAR 0: basic)
          "fp16x3": "catalog_score_x3b_kernel<32, 2, 0, 8, 2>"}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
                  (TABLE.get(precision, "catalog"), "pairs_table_" + precision), ("gather_rows", "gather_rows")):
