@@ -1467,6 +1467,19 @@ struct X6Slices {
 // (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
 // vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
 constexpr int X6N_FEATS_AT = 1;
+// A/B: the distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four
+// 16x16 tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each) instead of
+// two v_mfma_f32_16x16x4_f32 per block with half its K unused: half the f32 MFMA cycles
+#ifndef NAIS_X6N_DIST_4B
+#define NAIS_X6N_DIST_4B 0
+#endif
+constexpr bool X6N_DIST_4B = NAIS_X6N_DIST_4B != 0;
+#ifndef NAIS_X6N_COORDS_ONLY
+#define NAIS_X6N_COORDS_ONLY 0
+#endif
+__device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x1f32(a, b, c, 0, 0, 0);
+}
 // Tried and not kept (profiles/r5/prio_split, standalone table blocks, same process): static
 // priority 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4) 2.026 -> 2.014 ms at
 // D = H = 64, 7.474 -> 7.479 ms at D = H = 128; the D = 128 build's two entries at a quarter and
@@ -1564,7 +1577,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   }
   const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg / Adn
   // DIST: this lane's feature row of dist_layer (feature grp & 1, model.py:265 / 369)
-  const DistW dw = DIST ? load_distw<VAR>(p, grp & 1) : DistW{0.f, 0.f, 0.f, 0.f};
+  const DistW dw = DIST ? load_distw<VAR>(p, X6N_DIST_4B ? (grp >> 1) : (grp & 1)) : DistW{0.f, 0.f, 0.f, 0.f};
 
   float SAcur = 1.f;   // the W1 registers' current scale (rescaled per chunk)
 
@@ -1610,7 +1623,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     cout = cbase + 16 * (lane >> 5) + l16;
     vout = cout < clim;
     if constexpr (DIST) {   // lane group g computes feature g & 1 of candidate block g >> 1
-      const int64_t fc = cbase + 16 * (grp >> 1) + l16;
+                            // (4B: feature g >> 1 of candidate block g & 1)
+      const int64_t fc = cbase + 16 * (X6N_DIST_4B ? (grp & 1) : (grp >> 1)) + l16;
       const int64_t fcc = fc < clim ? fc : p.P - 1;
       if (coords) {
         fclat = coords[2 * fcc];
@@ -1677,7 +1691,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   auto feats = [&](int item) __attribute__((always_inline)) {
     item = std::min(item, jn_cur - 1);        // a stale step past the chunk (its MFMAs are unused)
     float ll0, ll1;
-    if (coords) {
+    if (NAIS_X6N_COORDS_ONLY || coords) {   // (timing-only A/B: 1 drops the latlon_mat branch)
       ll0 = (float)fabs(fclat - hco[2 * item]);
       ll1 = (float)fabs(fclon - hco[2 * item + 1]);
     } else {
@@ -1687,8 +1701,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
     const float f = dist_feature(dw, ll0, ll1) * Sd;   // exact power-of-two scaling
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
-    fN0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
-    fN1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
+    if constexpr (X6N_DIST_4B) {   // every lane: feature 0 / 1 of its candidate block g & 1
+      fN0 = __uint_as_float(r[0]);
+      fN1 = __uint_as_float(r[1]);
+    } else {
+      fN0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
+      fN1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
+    }
   };
 
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
@@ -1813,11 +1832,27 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (g + 1 < NG) aload(g + 1, a_nx);
         acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
         acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
-        if constexpr (DIST) {
+        if constexpr (DIST && !X6N_DIST_4B) {
           if (s == KS - 1) {   // the block's two distance columns: one exact fp32 K-step
             const float ad = Adn[(HPU * HC + 16 * m + l16) * 4 + grp];
             acc[m & 1][0] = mfma16f32(ad, fB0, acc[m & 1][0]);
             acc[m & 1][1] = mfma16f32(ad, fB1, acc[m & 1][1]);
+          }
+        }
+        if constexpr (DIST && X6N_DIST_4B) {
+          if ((m & 1) && s == 0) {   // blocks (m - 1, m): block m - 1's MFMAs are done, m's started
+            // lane group g supplies block g = (block m - 1 + (g >> 1), candidate block g & 1)
+            const float2 ad = *reinterpret_cast<const float2*>(Adn + (HPU * HC + 16 * (m - 1 + (grp >> 1)) + l16) * 4);
+            floatx16 c4 = __builtin_shufflevector(
+                __builtin_shufflevector(acc[0][0], acc[0][1], 0, 1, 2, 3, 4, 5, 6, 7),
+                __builtin_shufflevector(acc[1][0], acc[1][1], 0, 1, 2, 3, 4, 5, 6, 7),
+                0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+            c4 = mfma4b(ad.x, fB0, c4);
+            c4 = mfma4b(ad.y, fB1, c4);
+            acc[0][0] = __builtin_shufflevector(c4, c4, 0, 1, 2, 3);
+            acc[0][1] = __builtin_shufflevector(c4, c4, 4, 5, 6, 7);
+            acc[1][0] = __builtin_shufflevector(c4, c4, 8, 9, 10, 11);
+            acc[1][1] = __builtin_shufflevector(c4, c4, 12, 13, 14, 15);
           }
         }
         // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
