@@ -444,7 +444,7 @@ def table_kernel_name(precision, D, H, variant="basic"):
         return "catalog_score_kernel"
     if precision == "fp16x6" and D in (32, 64, 128) and H <= 128:
         return ("catalog_score_x6n_kernel (16x16x32 f16 MFMA%s)"
-                % (" + a 16x16x4 f32 K-step for the distance features" if dist else ""))
+                % (" + 16x16x1_4b f32 K-steps for the distance features" if dist else ""))
     if "pairsplit" in precision or (dist and (D > 64 or H > 64)):
         return "catalog_score_x3_kernel"
     if precision == "fp16x6" and (D > 64 or H > 64):

@@ -303,9 +303,9 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     din_k = D + (2 if dist else 0)      # the width the kernels multiply (padded)
     t_tab = J * NC * 2.0 * H * din_k * products / (1.3e14 if products == 1 else rate)
     if x6n and dist:
-        # the distance K-step: 2 v_mfma_f32_16x16x4_f32 (32 cycles each) per 16 hidden units beside
-        # the 12 * D / 32 f16 MFMAs (16 cycles each) of the block: 1 + 1 / (3 * D / 32) matrix time
-        t_tab *= 1.0 + 32.0 / (3.0 * D)
+        # the distance K-step: 2 v_mfma_f32_16x16x1_4b_f32 (32 cycles each) per PAIR of 16-hidden
+        # blocks beside their 2 * 12 * D / 32 f16 MFMAs (16 cycles each): 1 + 16 / (3 D) matrix time
+        t_tab *= 1.0 + 16.0 / (3.0 * D)
     if prior:
         t_tab += J * NC * 1.4e-11
     # gather rate per CU: ~72 GB/s while a block's e / e*s tables (block_bytes) mostly stay in the

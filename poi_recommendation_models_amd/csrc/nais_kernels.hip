@@ -1424,19 +1424,17 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 // v_permlane32_swap + one v_permlane16_swap for both candidate blocks at once; s = h_j . t_c comes
 // from a per-chunk s tile (items x candidates) that each wave parks in its own LDS slot in
 // [candidate][item] order, one ds_read per pair. The distance variants' two extra inputs
-// sigmoid(dist_layer(scale * |dlat, dlng|)) (model.py:265-267, 369-371) are one exact fp32
-// v_mfma_f32_16x16x4_f32 K-step per (hidden block, candidate block): A = the two W1 columns of the
-// block's hidden units (K rows 2, 3 zero), B = the pair's two features scaled by S (K rows 2, 3
-// zero). Each lane computes ONE feature of one pair -- lane group g: feature g & 1 of candidate
-// block g >> 1 -- and one v_permlane32_swap hands groups 0 / 1 both blocks' features.
+// sigmoid(dist_layer(scale * |dlat, dlng|)) (model.py:265-267, 369-371) are exact fp32 MFMA
+// K-steps: per pair of 16-hidden blocks, two v_mfma_f32_16x16x1_4b_f32 (one per feature) whose four
+// blocks are the pair's four 16 x 16 tiles (hidden block, candidate block); A = the W1 distance
+// column of the block's hidden units, B = the pair's feature scaled by S. Each lane computes ONE
+// feature of one pair -- lane group g: feature g >> 1 of candidate block g & 1 -- and one
+// v_permlane32_swap hands every lane both features of its block.
 // ---------------------------------------------------------------------------------------------
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ floatx4 mfma16n(half8 a, half8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ floatx4 mfma16f32(float a, float b, floatx4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 // the six fp16x6 products, smallest terms first (as mfma_pieces<3>)
 __device__ __forceinline__ floatx4 mfma16n_pieces(const half8 (&a)[3], const half8 (&b)[3], floatx4 c) {
@@ -1467,16 +1465,12 @@ struct X6Slices {
 // (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
 // vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
 constexpr int X6N_FEATS_AT = 1;
-// A/B: the distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four
-// 16x16 tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each) instead of
-// two v_mfma_f32_16x16x4_f32 per block with half its K unused: half the f32 MFMA cycles
-#ifndef NAIS_X6N_DIST_4B
-#define NAIS_X6N_DIST_4B 0
-#endif
-constexpr bool X6N_DIST_4B = NAIS_X6N_DIST_4B != 0;
-#ifndef NAIS_X6N_COORDS_ONLY
-#define NAIS_X6N_COORDS_ONLY 0
-#endif
+// The distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four 16x16
+// tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each; layout probed,
+// scripts/probes/mfma_4b_layout.hip, profiles/r5/d4b) instead of two v_mfma_f32_16x16x4_f32 per
+// block with half their K unused: region_distance table block 2.278 -> 2.251 ms (D = H = 64),
+// 8.193 -> 7.865 ms (D = H = 128), same process. (Dropping the latlon_mat branch of the feature
+// computation as well: 2.208 / 8.140 ms -- mixed, not pursued.)
 __device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_16x16x1f32(a, b, c, 0, 0, 0);
 }
@@ -1577,7 +1571,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   }
   const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg / Adn
   // DIST: this lane's feature row of dist_layer (feature grp & 1, model.py:265 / 369)
-  const DistW dw = DIST ? load_distw<VAR>(p, X6N_DIST_4B ? (grp >> 1) : (grp & 1)) : DistW{0.f, 0.f, 0.f, 0.f};
+  const DistW dw = DIST ? load_distw<VAR>(p, grp >> 1) : DistW{0.f, 0.f, 0.f, 0.f};
 
   float SAcur = 1.f;   // the W1 registers' current scale (rescaled per chunk)
 
@@ -1622,9 +1616,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // L ^ 16 alike): lane groups 0 / 2 carry e, groups 1 / 3 e * s
     cout = cbase + 16 * (lane >> 5) + l16;
     vout = cout < clim;
-    if constexpr (DIST) {   // lane group g computes feature g & 1 of candidate block g >> 1
-                            // (4B: feature g >> 1 of candidate block g & 1)
-      const int64_t fc = cbase + 16 * (X6N_DIST_4B ? (grp & 1) : (grp >> 1)) + l16;
+    if constexpr (DIST) {   // lane group g computes feature g >> 1 of candidate block g & 1
+      const int64_t fc = cbase + 16 * (grp & 1) + l16;
       const int64_t fcc = fc < clim ? fc : p.P - 1;
       if (coords) {
         fclat = coords[2 * fcc];
@@ -1691,7 +1684,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   auto feats = [&](int item) __attribute__((always_inline)) {
     item = std::min(item, jn_cur - 1);        // a stale step past the chunk (its MFMAs are unused)
     float ll0, ll1;
-    if (NAIS_X6N_COORDS_ONLY || coords) {   // (timing-only A/B: 1 drops the latlon_mat branch)
+    if (coords) {
       ll0 = (float)fabs(fclat - hco[2 * item]);
       ll1 = (float)fabs(fclon - hco[2 * item + 1]);
     } else {
@@ -1701,13 +1694,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     }
     const float f = dist_feature(dw, ll0, ll1) * Sd;   // exact power-of-two scaling
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
-    if constexpr (X6N_DIST_4B) {   // every lane: feature 0 / 1 of its candidate block g & 1
-      fN0 = __uint_as_float(r[0]);
-      fN1 = __uint_as_float(r[1]);
-    } else {
-      fN0 = grp < 2 ? __uint_as_float(r[0]) : 0.f;
-      fN1 = grp < 2 ? __uint_as_float(r[1]) : 0.f;
-    }
+    fN0 = __uint_as_float(r[0]);   // every lane: feature 0 / 1 of its candidate block g & 1
+    fN1 = __uint_as_float(r[1]);
   };
 
   // chunk unit u (item u / NHU, hidden slice u % NHU) into ring slot (grp_, it). With NE a multiple
@@ -1832,14 +1820,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         if (g + 1 < NG) aload(g + 1, a_nx);
         acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
         acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
-        if constexpr (DIST && !X6N_DIST_4B) {
-          if (s == KS - 1) {   // the block's two distance columns: one exact fp32 K-step
-            const float ad = Adn[(HPU * HC + 16 * m + l16) * 4 + grp];
-            acc[m & 1][0] = mfma16f32(ad, fB0, acc[m & 1][0]);
-            acc[m & 1][1] = mfma16f32(ad, fB1, acc[m & 1][1]);
-          }
-        }
-        if constexpr (DIST && X6N_DIST_4B) {
+        if constexpr (DIST) {   // the two distance columns: one exact fp32 K-step per feature
           if ((m & 1) && s == 0) {   // blocks (m - 1, m): block m - 1's MFMAs are done, m's started
             // lane group g supplies block g = (block m - 1 + (g >> 1), candidate block g & 1)
             const float2 ad = *reinterpret_cast<const float2*>(Adn + (HPU * HC + 16 * (m - 1 + (grp >> 1)) + l16) * 4);
