@@ -1477,8 +1477,15 @@ __device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
 // Tried and not kept (profiles/r5/prio_split, standalone table blocks, same process): static
 // priority 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4) 2.026 -> 2.014 ms at
 // D = H = 64, 7.474 -> 7.479 ms at D = H = 128; the D = 128 build's two entries at a quarter and
-// three quarters of the step instead of both at its middle 7.474 -> 7.509 ms.
+// three quarters of the step instead of both at its middle 7.474 -> 7.509 ms. Packed fp32 VALU
+// (v_pk_fma_f32 for the two candidate blocks' epilogue chains, v_pk_mul_f32 in the build: 498 ->
+// 437 VALU per 4-item block at D = 64) 1.983 -> 1.998 ms at D = H = 64, 7.198 -> 7.228 ms at 128
+// (profiles/r5/pk): the block is not issue-bound.
 
+#ifndef NAIS_X6N_W1_VGPRS
+#define NAIS_X6N_W1_VGPRS 32   // W1 values a thread may hold in VGPRs (more: W1G). 16 (W1 from L2
+                               // at D = H = 128 too): 20 -> 23 spilled VGPRs there, so not that
+#endif
 template <int D, int MB, int NHU, bool DIST = false>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
@@ -1506,7 +1513,7 @@ struct CfgN {
   static constexpr int GQ = (NHU / GU) > 2 ? NHU / GU : 2;
   // W1 read from global memory (L2) at each build instead of held in VGPRs when a thread's
   // share of it would take more than 32 VGPRs (D = 128 with more than 128 hidden units)
-  static constexpr bool W1G = NHU * EPT * 8 > 32;
+  static constexpr bool W1G = NHU * EPT * 8 > NAIS_X6N_W1_VGPRS;
   static_assert(BYTES <= 160 * 1024, "x6n: LDS");
   static_assert((GQ * GU) % NHU == 0 && GQ % 2 == 0 && GQ <= 4, "x6n: a round of groups spans whole items");
 };
@@ -1692,7 +1699,11 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       ll0 = (float)llrow[2 * hj];
       ll1 = (float)llrow[2 * hj + 1];
     }
-    const float f = dist_feature(dw, ll0, ll1) * Sd;   // exact power-of-two scaling
+    // v_exp_f32 + v_rcp_f32 (1 ulp each) instead of the correctly rounded expf and IEEE division
+    // (region_distance table block 2.204 -> 2.175 ms, profiles/r5/pk): the feature is an MLP
+    // input, so an ulp of it moves the logit far below its own fp32 rounding
+    const float z = (ll0 * dw.scale) * dw.w0 + (ll1 * dw.scale) * dw.w1 + dw.b;
+    const float f = __builtin_amdgcn_rcpf(1.0f + __expf(-z)) * Sd;   // exact power-of-two scaling
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
     fN0 = __uint_as_float(r[0]);   // every lane: feature 0 / 1 of its candidate block g & 1
     fN1 = __uint_as_float(r[1]);

@@ -7,6 +7,8 @@
 #   pmc       SQ counter passes of the standalone pair-table block (scripts/bench_table.py; extra
 #             args go to bench_table.py, e.g. --dim 128 --hidden 128)
 #   configs   config 2 whole job, config 5 direct and one rank's 8-GPU config-5 pairs shard
+#   ab        one standalone pair-table A/B (scripts/bench_table.py; extra args go to it, e.g.
+#             --variant region_distance --lib pk0=build_ab/pk0.so); output appended to ab.txt
 #   emulate   one rank's column shard of an N = 2 / 4 / 8 config-4 job, then the real 2-rank
 #             process group over gloo on the one GPU
 # Every GPU step runs under its own timeout and the steps are chained: the first failure ends it.
@@ -51,6 +53,9 @@ case "$mode" in
     line $out/config5_direct.json
     timeout -k 10 600 python bench.py --config 5 --strategy pairs --emulate-world 8 --no-fp32-leg --no-gather-leg --no-train-leg --no-self-check --steps 1 --warmup 1 > $out/config5_pairs_shard8.json 2> $out/config5_pairs_shard8.err || { tail -20 $out/config5_pairs_shard8.err; exit 1; }
     line $out/config5_pairs_shard8.json ;;
+  ab)
+    timeout -k 10 400 python scripts/bench_table.py "$@" >> $out/ab.txt 2>&1 || { tail -5 $out/ab.txt; exit 1; }
+    grep "ms/block" $out/ab.txt | tail -8 ;;
   emulate)
     for N in 2 4 8; do
       timeout -k 10 300 python bench.py --emulate-world $N --no-fp32-leg --no-gather-leg --no-train-leg --no-cpu-baseline --no-self-check \
