@@ -1470,7 +1470,8 @@ constexpr int X6N_FEATS_AT = 1;
 // scripts/probes/mfma_4b_layout.hip, profiles/r5/d4b) instead of two v_mfma_f32_16x16x4_f32 per
 // block with half their K unused: region_distance table block 2.278 -> 2.251 ms (D = H = 64),
 // 8.193 -> 7.865 ms (D = H = 128), same process. (Dropping the latlon_mat branch of the feature
-// computation as well: 2.208 / 8.140 ms -- mixed, not pursued.)
+// computation as well: 2.208 / 8.140 ms -- mixed; the config-4 region_distance job without it
+// 0.631 / 0.637 s against 0.640 / 0.636 s interleaved, profiles/r5/llm -- not pursued.)
 __device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_16x16x1f32(a, b, c, 0, 0, 0);
 }

@@ -1181,6 +1181,8 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   // persistent: W1 staged once and db1 / dw2 / dist_layer grads kept in LDS across all of the
   // workgroup's units (row tile of GWT rows, slice of 32 items), flushed once; the dW1 tiles and the
   // history-row grads are flushed per unit (registers: the dW1 tiles are live in its last phase only)
+  TSTART();   // timing builds: phases 0 W1 + unit staging, 1 u cache, 2 du / db1 / dw2, 3 dx MFMA,
+             // 4 history / target row grads, 5 dW1 rounds, 6 dW1 atomics, 7 history-row atomics, 8 flush
   gm_stage_w<GWT>(a, s, g, Lb, tid);
   for (int f = tid; f < 2 * g.HP32 + 8; f += GWT * 64) Lb[g.o_gb + f] = 0.f;
   const int ntile = g.HB * g.DBX;
@@ -1200,6 +1202,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     gm_stage<GWT>(a, s, g, L, tid, c0, j0, nj);
     for (int f = tid; f < 32 * g.HD; f += GWT * 64) L[g.o_gh + f] = 0.f;
     __syncthreads();
+    TMARK(0);
 
     // ---- recompute the forward, then du in place (C layout)
     floatx16 acc[HBM];
@@ -1233,6 +1236,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       ds = gl / Sb * e;                                           // dlogit / ds_cj
       da = ds * (sdot - a.beta * N / S);                          // dlogit / da_cj
     }
+    TMARK(1);
     const float kscale = a.drop.on ? a.drop.scale : 1.f;
     // du in place; db1 / dw2 as sums over the 32 pairs of each half (reduce-scatter), LDS atomics
   #pragma unroll
@@ -1258,6 +1262,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         atomicAdd(&L[g.o_gw + i], tz);
       }
     }
+    TMARK(2);
     // ---- dx = W1^T du (K-step (hb, r) = hidden unit crow(hb, r, hh): du straight from acc)
     constexpr int DBM = 4;
     floatx16 dx[DBM];
@@ -1284,6 +1289,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         }
       }
     }
+    TMARK(3);
     // ---- r = dx + ds: history-row grads (LDS atomics per item) and the target-row grad
   #pragma unroll
     for (int q = 0; q < DBM; ++q) {
@@ -1329,6 +1335,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         if (lane == 0 && live) atomicAdd(&L[g.o_gd + k], t);
       }
     }
+    TMARK(4);
     constexpr int OWN = (20 + GWT - 1) / GWT;   // dW1 tiles per wave: <= 4 hidden x 5 input blocks
     floatx16 gw[OWN];
 #pragma unroll
@@ -1366,6 +1373,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       }
       __syncthreads();
     }
+    TMARK(5);
     // ---- the unit's dW1 tiles
   #pragma unroll
     for (int q = 0; q < OWN; ++q) {
@@ -1378,6 +1386,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
         if (i < s.H && d < s.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * s.DIN + d], gw[q][r]);
       }
     }
+    TMARK(6);
     // ---- the unit's history-row grads (the last dW1 round's barrier ordered every LDS atomic)
     for (int f = tid; f < nj * s.D; f += GWT * 64) {
       const int jj = f / s.D, d = f % s.D;
@@ -1386,6 +1395,7 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
       if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], v);
       else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], v);
     }
+    TMARK(7);
   };
   if constexpr (GM_BWD_PERSIST) {
     for (int64_t un = blockIdx.x; un < units; un += gridDim.x) unit(un);
@@ -1399,6 +1409,8 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
     unsafeAtomicAdd(&gr.w2[i], Lb[g.o_gw + i]);
   }
   if (s.DIN > s.D && tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], Lb[g.o_gd + tid]);
+  TMARK(8);
+  TFLUSH();
 }
 
 size_t g_lds_bytes(const GArgs& a, bool backward, int gw = GW) {
@@ -1649,6 +1661,8 @@ int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64
 
 #ifndef NAIS_GM_TAIL
 #define NAIS_GM_TAIL 4   // rows per workgroup of the short-slice launches; 0 = one launch each
+// (config-3 step at D = H = 128, interleaved: 4 rows 0.487 / 0.485 ms, 2 rows 0.558 / 0.566, 6 rows
+// 0.497 / 0.497, 8 rows 0.498 / 0.497 -- profiles/r5/train_tail)
 #endif
 // The general kernels' units are (row tile, 32-item slice) workgroups, one per CU (LDS). When the
 // short last slice (n % 32 items) pushes the unit count into one more round of workgroups over the
