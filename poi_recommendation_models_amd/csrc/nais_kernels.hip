@@ -1409,7 +1409,7 @@ catalog_score_x3b_kernel(DevParams p, const int64_t* __restrict__ indptr,
 }
 
 // ---------------------------------------------------------------------------------------------
-// The fp16x6 item-side kernel on v_mfma_f32_16x16x32_f16 ("x6n", D in {32, 64, 128}, H <= 128 in
+// The fp16x6 item-side kernel on v_mfma_f32_16x16x32_f16 ("x6n", D in {32, 64, 128}, H <= 256 in
 // hidden-unit slices, every variant: basic, region, region_distance, distance): the x3b
 // factorisation A_j t_c, the same six products of exact hi / mid / lo f16 pieces, the same per-wave
 // candidate scale and pipelined epilogue, in 16 x 16 output tiles:
@@ -1580,6 +1580,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   const float Wmax = block_max_n<NW>(wmax, red);   // its barriers also publish Eimg / Adn
   // DIST: this lane's feature row of dist_layer (feature grp & 1, model.py:265 / 369)
   const DistW dw = DIST ? load_distw<VAR>(p, grp >> 1) : DistW{0.f, 0.f, 0.f, 0.f};
+  // -log2(e) * (scale * w0, scale * w1, b): the feature's exponent as two FMAs
+  const float fk0 = -1.44269504f * (dw.scale * dw.w0), fk1 = -1.44269504f * (dw.scale * dw.w1);
+  const float fk2 = -1.44269504f * dw.b;
 
   float SAcur = 1.f;   // the W1 registers' current scale (rescaled per chunk)
 
@@ -1703,8 +1706,10 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // v_exp_f32 + v_rcp_f32 (1 ulp each) instead of the correctly rounded expf and IEEE division
     // (region_distance table block 2.204 -> 2.175 ms, profiles/r5/pk): the feature is an MLP
     // input, so an ulp of it moves the logit far below its own fp32 rounding
-    const float z = (ll0 * dw.scale) * dw.w0 + (ll1 * dw.scale) * dw.w1 + dw.b;
-    const float f = __builtin_amdgcn_rcpf(1.0f + __expf(-z)) * Sd;   // exact power-of-two scaling
+    // (the exponent as two FMAs with -log2(e) and the scale folded in: block 2.198 -> 2.183 ms, the
+    // config-4 region_distance job 0.631 / 0.629 / 0.631 -> 0.626 / 0.631 / 0.627 s interleaved,
+    // profiles/r5/fold); S = Sd is an exact power of two
+    const float f = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(ll0, fk0, __builtin_fmaf(ll1, fk1, fk2)))) * Sd;
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(f), __float_as_uint(f), false, false);
     fN0 = __uint_as_float(r[0]);   // every lane: feature 0 / 1 of its candidate block g & 1
     fN1 = __uint_as_float(r[1]);
@@ -2713,7 +2718,7 @@ int launch_catalog_x3(const DevParams& d, const int64_t* indptr, const int64_t* 
 }
 
 // the 16x16x32 item-side kernel (x6n) instead of x3b / the per-pair split kernel for every fp16x6
-// shape it covers: D in {32, 64, 128}, H <= 128, every variant (the distance variants since round 5).
+// shape it covers: D in {32, 64, 128}, H <= 256, every variant (the distance variants since round 5).
 // Round-4 A/B against x3b at config 4: standalone 512-column table block 2.179 -> 1.990 ms, the job
 // 623 -> 601 ms (profiles/r4/x6n); at D = H = 128 against the per-pair split kernel: config-5 direct
 // 6.35e7 -> 7.32e7 pairs/s (profiles/r4/d128). The A/B switch is gone; x3b keeps fp16x3.

@@ -9,6 +9,9 @@
 #   configs   config 2 whole job, config 5 direct and one rank's 8-GPU config-5 pairs shard
 #   ab        one standalone pair-table A/B (scripts/bench_table.py; extra args go to it, e.g.
 #             --variant region_distance --lib pk0=build_ab/pk0.so); output appended to ab.txt
+#   abjob     the config-4 pairs job of one variant (scripts/bench_variant.py, all columns on this
+#             GPU) per library, interleaved: scripts/gpu_run.sh abjob TAG VARIANT base NAME ...
+#             (base = the in-tree library, NAME = build_ab/NAME.so)
 #   emulate   one rank's column shard of an N = 2 / 4 / 8 config-4 job, then the real 2-rank
 #             process group over gloo on the one GPU
 # Every GPU step runs under its own timeout and the steps are chained: the first failure ends it.
@@ -56,6 +59,15 @@ case "$mode" in
   ab)
     timeout -k 10 400 python scripts/bench_table.py "$@" >> $out/ab.txt 2>&1 || { tail -5 $out/ab.txt; exit 1; }
     grep "ms/block" $out/ab.txt | tail -8 ;;
+  abjob)
+    variant=$1; shift; i=0
+    for v in "$@"; do
+      i=$((i+1))
+      if [ $v = base ]; then L=poi_recommendation_models_amd/libnais_hip.so; else L=build_ab/$v.so; fi
+      NAIS_HIP_LIB=$L timeout -k 10 300 python scripts/bench_variant.py --variant $variant --num-users 50000 --num-pois 100000 \
+        --dim 64 --hidden 64 --emulate-world 1 --skip direct --steps 2 > $out/${i}_$v.json 2> $out/${i}_$v.err || { tail -5 $out/${i}_$v.err; exit 1; }
+      echo $v $(python -c "import json,sys; print(json.load(open(sys.argv[1]))['shard']['seconds_per_rank_step'])" $out/${i}_$v.json)
+    done ;;
   emulate)
     for N in 2 4 8; do
       timeout -k 10 300 python bench.py --emulate-world $N --no-fp32-leg --no-gather-leg --no-train-leg --no-cpu-baseline --no-self-check \
