@@ -1483,6 +1483,12 @@ __device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
 // 437 VALU per 4-item block at D = 64) 1.983 -> 1.998 ms at D = H = 64, 7.198 -> 7.228 ms at 128
 // (profiles/r5/pk): the block is not issue-bound.
 
+#ifndef NAIS_X6N_EPI_PREFETCH
+#define NAIS_X6N_EPI_PREFETCH 1
+#endif
+#ifndef NAIS_X6N_EPI_REGS
+#define NAIS_X6N_EPI_REGS 1
+#endif
 #ifndef NAIS_X6N_W1_VGPRS
 #define NAIS_X6N_W1_VGPRS 32   // W1 values a thread may hold in VGPRs (more: W1G). 16 (W1 from L2
                                // at D = H = 128 too): 20 -> 23 spilled VGPRs there, so not that
@@ -1784,8 +1790,18 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   static_assert(MB % 2 == 0, "x6n: block parity is compile-time");
   floatx4 acc[2][2];
   float apc0 = 0.f, apc1 = 0.f;
-  auto epi = [&](const float* ewb, const floatx4 (&a)[2], float& t0, float& t1) __attribute__((always_inline)) {
-    const float4 w4 = *reinterpret_cast<const float4*>(ewb + 4 * grp);
+  // one hidden slice (NHU == 1, no distance columns, D <= 64): this lane's S*b1 / w2/S rows of
+  // every block in VGPRs, loaded once per chunk, instead of an LDS read -- and its lgkmcnt(0) wait,
+  // which also drained the next group's A reads -- at every block's start and epilogue: D = H = 64
+  // 197 -> 233 VGPRs, table block 1.982 -> 1.905 ms, config-4 job 0.603 -> 0.597 s interleaved
+  // (profiles/r5/er). (D = 128 would spill; the distance variants sit at 245 VGPRs already.)
+  constexpr bool ER = NAIS_X6N_EPI_REGS && NHU == 1 && !DIST && D <= 64;
+  float4 breg[ER ? MB : 1], wreg[ER ? MB : 1];
+  auto wld = [&](const float* ewb, int m) __attribute__((always_inline)) {
+    if constexpr (ER) return wreg[m];
+    else return *reinterpret_cast<const float4*>(ewb + 4 * grp);
+  };
+  auto epi = [&](const float4 w4, const floatx4 (&a)[2], float& t0, float& t1) __attribute__((always_inline)) {
     t0 = __builtin_fmaf(w4.x, relu_bits(a[0][0]), t0);
     t0 = __builtin_fmaf(w4.y, relu_bits(a[0][1]), t0);
     t0 = __builtin_fmaf(w4.z, relu_bits(a[0][2]), t0);
@@ -1813,6 +1829,21 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         a[q] = *reinterpret_cast<const half8*>(&u4);
       }
     };
+    // EP: the LDS reads of S*b1 / w2/S issued one group ahead of their use, before that group's A
+    // reads, so the wait for them is a counted one that leaves the A reads in flight (where ER does
+    // not apply; lgkmcnt(0) waits per hot block 22 -> 13 at D = H = 128: block 7.478 -> 7.404 ms,
+    // region_distance 2.200 -> 2.180 ms, its config-4 job 0.620 -> 0.617 s, profiles/r5/ep)
+    constexpr bool EP = !ER && NAIS_X6N_EPI_PREFETCH;
+    float4 bnx = {0.f, 0.f, 0.f, 0.f}, wnx = {0.f, 0.f, 0.f, 0.f};
+    auto eload = [&](int g) __attribute__((always_inline)) {   // what group g's consumers need
+      const int m = g / KS, s = g % KS;
+      if (s == 0) bnx = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
+      if (s == EG) wnx = *reinterpret_cast<const float4*>((m == 0 ? ewp : ewc + 16 * (m - 1)) + 4 * grp);
+    };
+    if constexpr (EP) {
+      if (MMA) eload(0);
+      else wnx = *reinterpret_cast<const float4*>(ewp + 4 * grp);   // the drain step: its epilogue only
+    }
     half8 a_nx[3];
     if (MMA) aload(0, a_nx);
     if constexpr (DIST && MMA && HC == 0) {   // the item's features (formed one item ahead)
@@ -1822,9 +1853,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int m = g / KS, s = g % KS;
+      const float4 wcur = wnx;   // EP: this group's epilogue row (if it has one), read a group ago
       if (MMA) {
         if (s == 0) {   // the block's accumulators start at S*b1 (the MFMA's C operand)
-          const float4 b4 = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
+          float4 b4;
+          if constexpr (ER) b4 = breg[m];
+          else if constexpr (EP) b4 = bnx;
+          else b4 = *reinterpret_cast<const float4*>(ebc + 16 * m + 4 * grp);
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) {
             acc[m & 1][nb][0] = b4.x; acc[m & 1][nb][1] = b4.y;
@@ -1834,6 +1869,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         half8 a_[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) a_[q] = a_nx[q];
+        if constexpr (EP) {
+          if (g + 1 < NG) eload(g + 1);
+        }
         if (g + 1 < NG) aload(g + 1, a_nx);
         acc[m & 1][0] = mfma16n_pieces(a_, tb[0][s], acc[m & 1][0]);
         acc[m & 1][1] = mfma16n_pieces(a_, tb[1][s], acc[m & 1][1]);
@@ -1855,7 +1893,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
         }
         // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
         // against the last group; D = 64 unchanged -- profiles/r4/ab6)
+#ifndef NAIS_X6N_PROBE_NOBUILD   // timing probe only (wrong results): the in-step build's cost
         if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
+#endif
         // the next item's distance features, in the item's last unit (compile-time)
         if constexpr (DIST && HC == NHU - 1)
           if (g == std::min(X6N_FEATS_AT, NG - 1)) feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
@@ -1874,7 +1914,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       if (s != EG) continue;
       if (m == 0) {   // the previous unit's last block, then that unit is complete
         float ap0 = apc0, ap1 = apc1;
-        epi(ewp, acc[(MB - 1) & 1], ap0, ap1);
+        epi(EP ? wcur : wld(ewp, MB - 1), acc[(MB - 1) & 1], ap0, ap1);
         apc0 = 0.f;
         apc1 = 0.f;
         if constexpr (NHU == 1) {
@@ -1885,7 +1925,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
           if constexpr (HPV == NHU - 1) tail(prev < 0 ? 0 : prev / NHU, pa0, pa1, live);
         }
       } else if (MMA) {
-        epi(ewc + 16 * (m - 1), acc[(m - 1) & 1], apc0, apc1);
+        epi(EP ? wcur : wld(ewc + 16 * (m - 1), m - 1), acc[(m - 1) & 1], apc0, apc1);
       }
     }
   };
@@ -1973,6 +2013,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     build(0, std::integral_constant<int, 0>{}, 0, 0);
     if (GU == 2 && nunits > 1) build(1, std::integral_constant<int, 1 % NHU>{}, 0, 1);
     __syncthreads();   // group 0's fragments, this wave's S*b1 / w2/S and s tile published
+    if constexpr (ER) {
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        breg[m] = *reinterpret_cast<const float4*>(eb + 16 * m + 4 * grp);
+        wreg[m] = *reinterpret_cast<const float4*>(ew + 16 * m + 4 * grp);
+      }
+    }
     // one group: its units' steps, each building a unit of the next group (past the chunk's end a
     // clamped copy nobody reads) and finishing the previous unit; groups go in rounds of GQ (ring
     // slot GP & 1), so every step's hidden slices are compile-time. With GU = 2 and an odd unit
@@ -1991,7 +2038,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       };
       one(std::integral_constant<int, 0>{});
       if constexpr (GU == 2) one(std::integral_constant<int, 1>{});
+#ifndef NAIS_X6N_PROBE_NOBAR   // timing probe only (wrong results): the group barrier's cost
       __syncthreads();
+#endif
     };
     for (int g = 0; g < ngroups; g += C::GQ) {
       group(g, std::integral_constant<int, 0>{});
