@@ -1775,6 +1775,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(tab.e + row, (short)0, tab_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tab.es + row, (short)0, tab_bytes, 0x00020000);
     const bool odd = grp & 1;
+    // (the stores as non-temporal or sc1 instead of the default policy, so that the table block
+    // being written would not evict the stripe the gather reads from the Infinity Cache: config-4
+    // job 0.5968 / 0.5967 / 0.5966 s, base / nt / sc1 means of three interleaved runs, profiles/r5/nt)
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), re, odd ? (int)0x80000000 : off, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e * sv), rs, odd ? off : (int)0x80000000, 0, 0);
   };
@@ -1794,7 +1797,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // every block in VGPRs, loaded once per chunk, instead of an LDS read -- and its lgkmcnt(0) wait,
   // which also drained the next group's A reads -- at every block's start and epilogue: D = H = 64
   // 197 -> 233 VGPRs, table block 1.982 -> 1.905 ms, config-4 job 0.603 -> 0.597 s interleaved
-  // (profiles/r5/er). (D = 128 would spill; the distance variants sit at 245 VGPRs already.)
+  // (profiles/r5/er). (D = 128 would spill; the distance variants sit at 245 VGPRs already.) The
+  // tail's s / history-id reads and the build's history-row reads a group ahead as well: neutral
+  // (block 1.863 vs 1.855 / 1.858 ms without either, job 0.5964 / 0.5958 / 0.5961 s, profiles/r5/tp).
   constexpr bool ER = NAIS_X6N_EPI_REGS && NHU == 1 && !DIST && D <= 64;
   float4 breg[ER ? MB : 1], wreg[ER ? MB : 1];
   auto wld = [&](const float* ewb, int m) __attribute__((always_inline)) {
