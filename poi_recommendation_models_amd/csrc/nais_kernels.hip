@@ -1907,7 +1907,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       }
       if constexpr (D == 128) {
         // issue order of the group: the next group's A reads, then MFMAs with VALU between
-        // (D = H = 128 block 7.60 -> 7.46 ms; at D = 64 it costs 5 %, profiles/r4/ab6)
+        // (D = H = 128 block 7.60 -> 7.46 ms; at D = 64 it costs 5 %, profiles/r4/ab6; counting
+        // EP's extra read into the first set where a group has one: 7.171 -> 7.275 ms, profiles/r5/sep)
         if (MMA) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
