@@ -1464,7 +1464,10 @@ struct X6Slices {
 // The distance term as 16 VALU FMAs per 16-hidden block on the accumulators' initial values
 // (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
 // vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
-constexpr int X6N_FEATS_AT = 1;
+#ifndef NAIS_X6N_FEATS_AT
+#define NAIS_X6N_FEATS_AT 1
+#endif
+constexpr int X6N_FEATS_AT = NAIS_X6N_FEATS_AT;
 // The distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four 16x16
 // tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each; layout probed,
 // scripts/probes/mfma_4b_layout.hip, profiles/r5/d4b) instead of two v_mfma_f32_16x16x4_f32 per
