@@ -1464,10 +1464,12 @@ struct X6Slices {
 // The distance term as 16 VALU FMAs per 16-hidden block on the accumulators' initial values
 // (acc = S b1 + wd0 f0 + wd1 f1) instead of the f32 MFMA K-step: 2.256 vs 2.246 ms (D = 64), 8.017
 // vs 8.058 ms (D = 128) -- a wash, not kept (profiles/r5/dist_valu).
+// With the cheaper feature (v_exp / v_rcp, the folded exponent) group 3 wins at D = 64: table block
+// 2.093 / 2.075 / 2.077 ms and the config-4 job 0.616 / 0.614 / 0.612 s at groups 1 / 0 / 3
+// (profiles/r5/fa); D = 128 keeps group 1 (unmeasured since).
 #ifndef NAIS_X6N_FEATS_AT
-#define NAIS_X6N_FEATS_AT 1
+#define NAIS_X6N_FEATS_AT -1   // -1: 3 at D <= 64, 1 at D = 128
 #endif
-constexpr int X6N_FEATS_AT = NAIS_X6N_FEATS_AT;
 // The distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four 16x16
 // tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each; layout probed,
 // scripts/probes/mfma_4b_layout.hip, profiles/r5/d4b) instead of two v_mfma_f32_16x16x4_f32 per
@@ -1906,7 +1908,8 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
 #endif
         // the next item's distance features, in the item's last unit (compile-time)
         if constexpr (DIST && HC == NHU - 1)
-          if (g == std::min(X6N_FEATS_AT, NG - 1)) feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
+          if (g == std::min(NAIS_X6N_FEATS_AT >= 0 ? NAIS_X6N_FEATS_AT : (D <= 64 ? 3 : 1), NG - 1))
+            feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
       }
       if constexpr (D == 128) {
         // issue order of the group: the next group's A reads, then MFMAs with VALU between
