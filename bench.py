@@ -410,7 +410,7 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
         # slack lr * min(2, 2e-4 max|g| / |g|): the first step's lr * g / |g| amplifies the
         # gradient's rounding (tolerance 1e-4 max|g|) where |g| is small against the tensor's
         # largest (tests/_helpers.py::adagrad_slack)
-        bad, unexplained, worst_dev = 0, 0, 0.0
+        bad, unexplained, worst_dev, over_limit, per_tensor = 0, 0, 0.0, 0, {}
         for k, v in p0.items():
             g = r["grads"][k].reshape(v.shape)
             want, _ = train_oracle.adagrad(v, np.zeros_like(v), g, 0.01, 1)
@@ -422,32 +422,44 @@ def train_leg(dev, D, H, P=100_000, n=204, num_ng=4, steps=50, warmup=5, check=T
             miss = dev > plain
             bad += int(miss.sum())
             unexplained += int((dev > plain + slack).sum())
+            # as tests/_helpers.assert_params_close: at most 0.1 % of a tensor, and 32, may need
+            # the slack
+            over_limit += int(miss.sum()) > min(32, int(1e-3 * miss.size))
             if miss.any():
                 worst_dev = max(worst_dev, float(dev[miss].max()))
+                per_tensor[k] = {"count": int(miss.sum()), "size": int(miss.size),
+                                 "max_g_ratio": float(ga[miss].max() / max(ga.max(), 1e-300))}
         out["self_check"] = {"oracle": "oracle/train_oracle.py (float64, dropout mask injected)",
                              "loss": loss0, "oracle_loss": float(r["loss"]),
                              "loss_ok": abs(loss0 - float(r["loss"])) <= 1e-5,
                              "params_off_rtol_1e-4": bad, "params_beyond_adagrad_slack": unexplained,
+                             "slack_elements_by_tensor": per_tensor,
+                             "tensors_over_slack_limit": over_limit,
                              "max_dev_off": worst_dev,
-                             "params_ok": unexplained == 0,
+                             "params_ok": unexplained == 0 and over_limit == 0,
                              "seconds": round(time.perf_counter() - t0, 1)}
     del tr, opt, em, eopt, m
     torch.cuda.empty_cache()
     return out
 
 
-def table_kernel_name(precision, D, H, variant="basic"):
-    """The catalog kernel nais_pair_table runs for this shape (nais_kernels.hip's dispatch:
-    launch_catalog_x3b / launch_catalog_x3 / launch_catalog)."""
+def table_kernel_name(precision, D, H, variant="basic", mode="table"):
+    """The catalog kernel nais_pair_table (mode "table") or nais_score_catalog (mode "direct")
+    runs for this shape -- nais_kernels.hip's dispatch: pair_table_impl sends fp16x6 AND
+    fp16x6_pairsplit to launch_catalog_x6b, the direct route sends fp16x6_pairsplit to
+    launch_catalog_x6 (the per-pair split kernel); launch_catalog_x3b takes x6n for D in
+    {32, 64, 128} at any H <= 256 when NPC = 3."""
     dist = variant in ("region_distance", "distance")
     if precision == "fp32" or D < 16:
         return "catalog_score_kernel"
-    if precision == "fp16x6" and D in (32, 64, 128) and H <= 128:
+    fp16x6 = precision.startswith("fp16x6")
+    x6b = fp16x6 and (mode == "table" or precision == "fp16x6")
+    if x6b and D in (32, 64, 128) and H <= 256:
         return ("catalog_score_x6n_kernel (16x16x32 f16 MFMA%s)"
                 % (" + 16x16x1_4b f32 K-steps for the distance features" if dist else ""))
-    if "pairsplit" in precision or (dist and (D > 64 or H > 64)):
+    if precision.endswith("pairsplit") and not x6b:
         return "catalog_score_x3_kernel"
-    if precision == "fp16x6" and (D > 64 or H > 64):
+    if (dist or fp16x6) and (D > 64 or H > 64):
         return "catalog_score_x3_kernel"
     return "catalog_score_x3b_kernel"
 
@@ -680,7 +692,7 @@ def main():
             },
             "roofline": {
                 "kernel": ("catalog_score_x3_kernel" if "pairsplit" in a.precision
-                           else table_kernel_name(a.precision, D, H)) + " (nais_score_catalog)",
+                           else table_kernel_name(a.precision, D, H, mode="direct")) + " (nais_score_catalog)",
                 "bound": "mfma",
                 "achieved": achieved,
                 "peak": peak,

@@ -55,10 +55,18 @@ def build(force=False, extra=(), out=None, extra_for=None):
         objs.append(o)
         if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_time):
             todo.append((src, o, f))
-    if not todo and os.path.exists(OUT_) and all(os.path.getmtime(OUT_) >= os.path.getmtime(o) for o in objs):
+    # the link is keyed too: a sidecar next to the library records the objects it was linked
+    # from (their names carry the flag hashes), so a variant name reused with other -D flags, or
+    # a library linked from other objects, is relinked even when it is newer than the objects
+    stamp = OUT_ + ".objs"
+    linked = open(stamp).read() if os.path.exists(stamp) else None
+    if (not todo and os.path.exists(OUT_) and linked == "\n".join(objs)
+            and all(os.path.getmtime(OUT_) >= os.path.getmtime(o) for o in objs)):
         return OUT_
-    # the changed translation units compiled in parallel, then one link
-    procs = [(subprocess.Popen([hipcc(), *f, "-c", "-o", o + ".tmp", src], stdout=subprocess.PIPE,
+    # the changed translation units compiled in parallel, then one link; temporary names carry
+    # the pid, so concurrent builds with the same flags do not write the same file
+    tmp = f".{os.getpid()}.tmp"
+    procs = [(subprocess.Popen([hipcc(), *f, "-c", "-o", o + tmp, src], stdout=subprocess.PIPE,
                                stderr=subprocess.STDOUT, text=True), src, o) for src, o, f in todo]
     failed = []
     for pr, src, o in procs:
@@ -67,15 +75,18 @@ def build(force=False, extra=(), out=None, extra_for=None):
             sys.stderr.write(log)
             failed.append(os.path.basename(src))
         else:
-            os.replace(o + ".tmp", o)
+            os.replace(o + tmp, o)
     if failed:
         raise RuntimeError(f"hipcc failed on {failed}")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_ + ".tmp", *objs]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT_ + tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc link failed ({r.returncode}): {' '.join(cmd)}")
-    os.replace(OUT_ + ".tmp", OUT_)
+    os.replace(OUT_ + tmp, OUT_)
+    with open(stamp + tmp, "w") as fh:
+        fh.write("\n".join(objs))
+    os.replace(stamp + tmp, stamp)
     return OUT_
 
 

@@ -14,6 +14,7 @@ Parameters without such a record, or any parameter when weight_decay != 0, get t
 from __future__ import annotations
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _capi
 
@@ -78,4 +79,8 @@ class Adagrad(torch.optim.Optimizer):
                     _capi.check(lib.nais_adagrad(p.data_ptr(), s.data_ptr(), g.data_ptr(), p.numel(),
                                                  clr, group["weight_decay"], group["eps"], stream),
                                 "nais_adagrad")
+                # the kernels write p through its raw pointer; bump its version counter as an
+                # in-place torch op would, so version-keyed caches (model._score_params' padded
+                # copies) see the update
+                increment_version(p)
         return loss

@@ -226,21 +226,30 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     # the exchange: one all-gather of this rank's [n, k] block per array ([world * n, k], rank
     # order = ascending POI ranges), then the merge over the world * k candidates per user
     mark = _marker(events, dev)
-    if prior is not None:
-        gi = all_gather_cat(ids, group).view(world, n, k)
-        gk = all_gather_cat(out[2], group).view(world, n, k)
-    else:
-        # ONE all-gather of (int32 id, f32 score bits) pairs: 8 B per entry instead of 12 in two
-        # calls (POI ids < 2^31; -1 marks a short list) -- at config 4 and N = 8 each rank receives
-        # 7 x 50k x 50 x 8 B = 140 MB over the ring
-        pk = torch.stack([ids.to(torch.int32), sc.contiguous().view(torch.int32)], dim=-1)
-        g = all_gather_cat(pk, group).view(world, n, k, 2)
-        gi = g[..., 0].to(torch.int64)
-        gk = g[..., 1].contiguous().view(torch.float32)
+    gi, gk = exchange_blocks(ids, out[2] if prior is not None else sc, group,
+                             wide_ids=prior is not None or P > 2**31 - 1)
     mark("allgather")
     res = merge_topk_f64(gi, gk, k) if prior is not None else merge_topk(gi, gk, k)
     mark("merge")
     return res
+
+
+def exchange_blocks(ids, keys, group=None, wide_ids=False):
+    """All-gather every rank's [n, k] top-k block: ids (int64 POI ids, -1 = short list) and keys
+    (f32 scores, or the prior route's f64 keys) -> ([world, n, k] int64, [world, n, k] keys), rank
+    order = ascending POI ranges. f32 keys with int32-representable ids travel as ONE all-gather of
+    (int32 id, f32 score bits) pairs: 8 B per entry instead of 12 in two calls -- at config 4 and
+    N = 8 each rank receives 7 x 50k x 50 x 8 B = 140 MB over the ring. `wide_ids` (f64 keys, or a
+    catalog of 2^31 POIs or more, whose ids an int32 would wrap) takes two gathers instead."""
+    world = _world(group)
+    n, k = ids.shape
+    if wide_ids or keys.dtype != torch.float32:
+        gi = all_gather_cat(ids.contiguous(), group).view(world, n, k)
+        gk = all_gather_cat(keys.contiguous(), group).view(world, n, k)
+        return gi, gk
+    pk = torch.stack([ids.to(torch.int32), keys.contiguous().view(torch.int32)], dim=-1)
+    g = all_gather_cat(pk, group).view(world, n, k, 2)
+    return g[..., 0].to(torch.int64), g[..., 1].contiguous().view(torch.float32)
 
 
 def _marker(events, dev):

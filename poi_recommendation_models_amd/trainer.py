@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import numpy as np
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _capi
 from .catalog import device_csr
@@ -186,6 +187,7 @@ class NAISTrainer:
                 _capi.stream_handle(self.dev))
         if not (self.region or self.distance):
             _capi.check(lib.nais_train_step(prm, self._opt_struct(), *args), "nais_train_step")
+            self._bump_versions()
             return
         os_ = _capi.NaisAdagradSide()
         if self.region:
@@ -196,7 +198,15 @@ class NAISTrainer:
             os_.sum_dist_b = self.sums["dist_layer.bias"].data_ptr()
             os_.grad_dist = self._g_dist.data_ptr()
         _capi.check(lib.nais_train_step_ex(prm, sd, self._opt_struct(), os_, *args), "nais_train_step_ex")
+        self._bump_versions()
         del keep
+
+    def _bump_versions(self):
+        """The fused step writes the parameters through raw pointers: bump their version counters
+        as an in-place torch op would, so version-keyed caches (model._score_params' padded copies
+        for embed widths off the kernels' native set) are rebuilt before the next scoring call."""
+        for q in self.model.parameters():
+            increment_version(q)
 
     def epoch(self, users=None, shuffle=True):
         """One pass of run.py:96-109 over `users` (default: every user, shuffled as run.py:96-97).

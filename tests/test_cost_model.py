@@ -60,3 +60,24 @@ def test_distance_variants_take_the_x6n_steps():
     m.VARIANT = 0            # NAIS_basic at D = 66: padded to 128, twice the table FLOPs
     n = auto_table_cus(m, 100_000, 100_000, 5_030_351, 256, False)
     assert n % 8 == 0 and n > 152
+
+
+@pytest.mark.parametrize("precision,D,H,mode,want", [
+    ("fp16x6", 64, 64, "table", "x6n"),
+    ("fp16x6", 64, 64, "direct", "x6n"),
+    ("fp16x6_pairsplit", 64, 64, "table", "x6n"),     # pair_table_impl: both fp16x6 -> x6b
+    ("fp16x6_pairsplit", 64, 64, "direct", "x3"),     # score_catalog: pairsplit -> launch_catalog_x6
+    ("fp16x6", 64, 200, "table", "x6n"),              # 128 < H <= 256 runs on x6n
+    ("fp16x6", 128, 256, "direct", "x6n"),
+    ("fp16x6", 16, 64, "table", "x3b"),               # D = 16: no x6n instance
+    ("fp16x3", 64, 64, "table", "x3b"),
+    ("fp16x3_pairsplit", 64, 64, "direct", "x3"),
+    ("fp32", 64, 64, "table", "catalog_score_kernel"),
+    ("fp16x6", 8, 64, "table", "catalog_score_kernel"),
+])
+def test_bench_kernel_label_mirrors_dispatch(precision, D, H, mode, want):
+    """bench.py's roofline names the kernel nais_kernels.hip dispatches."""
+    import bench
+    name = bench.table_kernel_name(precision, D, H, mode=mode)
+    want = want if want.startswith("catalog") else f"catalog_score_{want}_kernel"
+    assert name.split(" ")[0] == want

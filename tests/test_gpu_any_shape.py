@@ -142,7 +142,7 @@ def test_training_step_100x100_vs_oracle():
     for k, q in m.named_parameters():
         g = r["grads"][k].reshape(p[k].shape)
         want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), g, 0.01, 1)
-        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g, 0.01))
+        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g, 0.01), g=g)
     # eval-mode scoring of the trained module runs from the padded copies of the new parameters
     m.eval()
     h0 = hist[0][:5]
@@ -150,3 +150,51 @@ def test_training_step_100x100_vs_oracle():
     q = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
     ref, _ = nais_oracle.forward_basic(q, np.tile(h0, (6, 1)), np.arange(6))
     assert np.max(np.abs(got - ref)) <= SCORE_ATOL
+
+
+@pytest.mark.parametrize("writer", ["adagrad", "trainer"])
+def test_padded_copies_follow_native_optimizer_writes(writer):
+    """the padded copies for an embed width off the native set (D = 100) are
+    keyed on the parameters' version counters; optim.Adagrad and NAISTrainer write the parameters
+    through raw device pointers and must bump those counters. The run.py flow -- score, train,
+    score again (validation inside the epoch loop, run.py:112-116) -- must score the NEW
+    parameters: checked against the numpy oracle after each writer."""
+    from poi_recommendation_models_amd import optim
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_catalog
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    from test_gpu_train import _batch, _csr, _params, _trainer
+    from test_gpu_train import _model as _train_model
+    P, D, H = 1500, 100, 48
+    data = make_checkins(3, P, 30, seed=8)
+    m = _train_model(_params(P, D, H, seed=21))
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, torch.device(DEV))
+
+    def check(tag):
+        m.eval()
+        got = score_catalog(m, csr, range(3)).cpu().numpy()
+        q = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+        worst = 0.0
+        for u in range(3):
+            cand, ref = nais_oracle.catalog_scores_basic(q, data.history(u), P)
+            worst = max(worst, float(np.max(np.abs(got[u][cand] - ref))))
+        assert worst <= SCORE_ATOL, (tag, worst)
+        return q
+
+    before = check("before")
+    hist, tgt, labels = _batch(P, 40, 4, seed=3)
+    m.train()
+    if writer == "adagrad":
+        o = optim.Adagrad(m.parameters(), lr=0.05)
+        for q in m.parameters():
+            q.grad = None
+        pred = m(torch.as_tensor(hist).to(DEV), torch.as_tensor(tgt).to(DEV))
+        m.loss_func(pred, torch.as_tensor(labels).to(DEV)).backward()
+        o.step()
+    else:
+        tr = _trainer(m, _csr(3, P, 30, seed=4), lr=0.05)
+        tr.step(torch.as_tensor(hist).to(DEV), torch.as_tensor(tgt).to(DEV),
+                torch.as_tensor(labels).to(DEV))
+        tr.finish()
+    after = check("after " + writer)
+    moved = max(float(np.max(np.abs(after[k] - before[k]))) for k in before)
+    assert moved > 1e-3                       # the parameters did change

@@ -234,6 +234,7 @@ def test_training_loop_matches_oracle(D, H, drop, monkeypatch):
     ref = {k: v.copy() for k, v in p.items()}
     st = {k: np.zeros_like(v) for k, v in p.items()}
     slack = {k: np.zeros(v.shape) for k, v in p.items()}
+    first_g = {}
     for step in range(1, 4):
         hist, data, labels = _batch(P, n, 4, seed=100 + step)
         seed = 4242 + step
@@ -247,12 +248,13 @@ def test_training_loop_matches_oracle(D, H, drop, monkeypatch):
         for k in NAMES:
             g = r["grads"][k].reshape(ref[k].shape)
             slack[k] += adagrad_slack(g, 0.01)
+            first_g.setdefault(k, g)
             ref[k], st[k] = train_oracle.adagrad(ref[k], st[k], g, 0.01, step)
     # Adagrad divides by sqrt(sum g^2): an element whose gradient is small against the tensor's
     # largest amplifies the gradient's fp32 rounding (a sign flip at the first step moves it 2 lr);
     # each element may differ by its own accumulated slack only (assert_params_close prints them).
     for k, q in m.named_parameters():
-        assert_params_close(k, q.detach().cpu().numpy(), ref[k], slack[k])
+        assert_params_close(k, q.detach().cpu().numpy(), ref[k], slack[k], g=first_g[k])
 
 
 # ------------------------------------------------------------------ fused step + device batches
@@ -355,7 +357,7 @@ def test_fused_step_matches_dropin(D, H):
             g = grads[k]
             sl = 0.0 if g is None else adagrad_slack(g, 0.01)
             assert_params_close(f"step {step} {k}", a.detach().cpu().numpy(), b.detach().cpu().numpy(),
-                                sl, rtol=1e-5, atol=1e-6)
+                                sl, rtol=1e-5, atol=1e-6, g=g)
             np.testing.assert_allclose(tr.sums[k].cpu().numpy(), ob.state[b]["sum"].cpu().numpy(),
                                        rtol=1e-3, atol=1e-9)
     assert tr.finish() > 0
@@ -396,7 +398,8 @@ def test_fused_step_oracle(wd, D, H):
     for k, q in m.named_parameters():
         g = r["grads"][k].reshape(p[k].shape)
         want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), g, 0.02, 1, weight_decay=wd)
-        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g + wd * p[k], 0.02))
+        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g + wd * p[k], 0.02),
+                            g=g + wd * p[k])
 
 
 def test_fused_step_config3_split_vs_oracle():
@@ -415,7 +418,7 @@ def test_fused_step_config3_split_vs_oracle():
     for k, q in m.named_parameters():
         g = r["grads"][k].reshape(p[k].shape)
         want, _ = train_oracle.adagrad(p[k], np.zeros_like(p[k]), g, 0.02, 1)
-        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g, 0.02))
+        assert_params_close(k, q.detach().cpu().numpy(), want, adagrad_slack(g, 0.02), g=g)
 
 
 @pytest.mark.parametrize("D,H", [(16, 16), (128, 128)])
@@ -464,6 +467,7 @@ def test_fused_step_config3_full_catalog(D, H, wd):
     ref = {k: v.copy() for k, v in p.items()}
     st = {k: np.zeros_like(v) for k, v in ref.items()}
     slack = {k: np.zeros(v.shape) for k, v in ref.items()}
+    first_g = {}
     total = 0.0
     for step in (1, 2):
         hist, data, labels = _batch(P, n, 4, seed=40 + step)
@@ -479,11 +483,12 @@ def test_fused_step_config3_full_catalog(D, H, wd):
         for k in NAMES:
             g = r["grads"][k].reshape(ref[k].shape)
             slack[k] += adagrad_slack(g + wd * ref[k], 0.02)      # the gradient Adagrad sees
+            first_g.setdefault(k, g + wd * ref[k])
             ref[k], st[k] = train_oracle.adagrad(ref[k], st[k], g, 0.02, step, weight_decay=wd)
     touched = np.zeros(P, bool)
     for k, q in m.named_parameters():
         got = q.detach().cpu().numpy()
-        assert_params_close(k, got, ref[k], slack[k])
+        assert_params_close(k, got, ref[k], slack[k], g=first_g[k])
         if k.startswith("embed") and wd == 0.0:   # untouched rows: bit-identical to the start
             touched[:] = False
             for step in (1, 2):

@@ -512,3 +512,16 @@ def test_prior_route_respects_merge_cap(monkeypatch, world, k, route):
     X = sp.csr_matrix((np.ones(3), np.array([0, 1, 2]), np.array([0, 3])), shape=(1, 4000))
     sharding.distributed_topk(Model(), X, 1, k, prior=(0.05, -1.3, 0.2, None))
     assert taken == [route]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_every_collective_world_n_gloo(tmp_path, world):
+    """tests/collectives_worker.py over gloo at world 2 / 3 (fresh torch.distributed.run children):
+    every collective sharding.py issues -- the packed int32 / wide / f64 top-k exchanges, the f64
+    row all-gather, the int64 MAX / MIN all-reduces, the module broadcast, the sharded table load
+    with P not divisible by the world -- bit-identical to its numpy restatement. The GPU test
+    (tests/test_gpu_rccl.py) runs the same worker over RCCL."""
+    import _collectives
+    res = _collectives.run(world, "gloo", str(tmp_path / "gloo.npz"))
+    names = _collectives.assert_matches_expected(res, world, device_merges=False)
+    assert len(names) == 17
