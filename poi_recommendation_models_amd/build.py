@@ -7,7 +7,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("nais_kernels.hip", "nais_train.hip", "nais_new4.hip", "nais_pairs.hip", "nais_dot.hip", "nais_disent.hip")]
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("nais_kernels.hip", "nais_train.hip", "nais_new4.hip", "nais_pairs.hip", "nais_dot.hip", "nais_disent.hip", "nais_generic.hip")]
 SRC = SRCS[0]
 OUT = os.path.join(HERE, "libnais_hip.so")
 ARCH = os.environ.get("NAIS_OFFLOAD_ARCH", "gfx950")

@@ -2655,6 +2655,9 @@ int check_launch(const char* what) {
 
 struct Shape {
   int DH, HB;
+  // the generic-shape kernels (nais_generic.hip) instead of the tuned ones: nais_forward (fwd),
+  // nais_score_catalog / nais_score_topk (cat), nais_pair_table (tab)
+  bool gen_fwd, gen_cat, gen_tab;
 };
 
 int validate(const nais_params_t* p, Shape* sh) {
@@ -2667,9 +2670,9 @@ int validate(const nais_params_t* p, Shape* sh) {
   if (p->num_pois <= 0) return fail(NAIS_E_INVALID, "num_pois must be > 0");
   if (p->num_pois > 65535ll * 256) return fail(NAIS_E_UNSUPPORTED, "num_pois > 16.7M (grid.y limit)");
   const int D = p->embed_dim;
-  if (D <= 0 || D % 8 != 0 || D > 128)
-    return fail(NAIS_E_UNSUPPORTED, "embed_dim must be a multiple of 8 in [8, 128]");
-  if (p->hidden <= 0 || p->hidden > 256) return fail(NAIS_E_UNSUPPORTED, "hidden must be in [1, 256]");
+  if (D <= 0 || D > 256)
+    return fail(NAIS_E_UNSUPPORTED, "embed_dim must be in [1, 256] (the generic kernels' LDS budget)");
+  if (p->hidden <= 0) return fail(NAIS_E_UNSUPPORTED, "hidden must be >= 1");
   if (p->variant == NAIS_VARIANT_BASIC) {
     if (p->item_dim != D || p->din != D) return fail(NAIS_E_INVALID, "basic: item_dim == din == embed_dim");
   } else if (p->variant == NAIS_VARIANT_DISTANCE) {
@@ -2677,7 +2680,7 @@ int validate(const nais_params_t* p, Shape* sh) {
       return fail(NAIS_E_INVALID, "distance: item_dim == embed_dim, din == embed_dim + 2");
     if (!p->dist_w || !p->dist_b) return fail(NAIS_E_INVALID, "distance needs dist_layer weight and bias");
   } else {
-    if (p->item_dim != D / 2 || p->region_dim != D / 2)
+    if (D % 2 != 0 || p->item_dim != D / 2 || p->region_dim != D / 2)
       return fail(NAIS_E_INVALID, "region variants: item_dim == region_dim == embed_dim/2");
     if (!p->embed_region || p->num_regions <= 0) return fail(NAIS_E_INVALID, "missing embed_region");
     const int want = D + (p->variant == NAIS_VARIANT_REGION_DISTANCE ? 2 : 0);
@@ -2685,13 +2688,20 @@ int validate(const nais_params_t* p, Shape* sh) {
     if (p->variant == NAIS_VARIANT_REGION_DISTANCE && (!p->dist_w || !p->dist_b))
       return fail(NAIS_E_INVALID, "region_distance needs dist_layer weight and bias");
   }
-  sh->DH = D / 2;
+  // the tuned kernels: embed widths 8 / 16 / 32 / 64 / 128 (the MFMA K tiles), hidden <= 256 in
+  // the forward and the fp16x6 item-side kernel (D 32 / 64 / 128), <= 128 in the other catalog
+  // kernels; every other shape takes the generic kernels (exact fp32)
+  const bool native = D == 8 || D == 16 || D == 32 || D == 64 || D == 128;
+  const bool x6n = D == 32 || D == 64 || D == 128;
+  sh->gen_fwd = !native || p->hidden > 256;
+  sh->gen_cat = sh->gen_fwd || (p->hidden > 128 && !(x6n && p->precision == NAIS_PRECISION_FP16X6));
+  sh->gen_tab = sh->gen_fwd || (p->hidden > 128 && !(x6n && (p->precision == NAIS_PRECISION_FP16X6 ||
+                                                            p->precision == NAIS_PRECISION_FP16X6_PAIRSPLIT)));
+  sh->DH = native ? D / 2 : 4;
   int hb = (p->hidden + 31) / 32;   // 32-hidden blocks: 1, 2, 4 or 8 (hidden > 128)
   if (hb == 3) hb = 4;
   if (hb > 4) hb = 8;
   sh->HB = hb;
-  if (sh->DH != 4 && sh->DH != 8 && sh->DH != 16 && sh->DH != 32 && sh->DH != 64)
-    return fail(NAIS_E_UNSUPPORTED, "embed_dim must be one of 8, 16, 32, 64, 128");
   return NAIS_OK;
 }
 
@@ -2981,6 +2991,9 @@ int32_t nais_forward(const nais_params_t* params, const int64_t* hist, int64_t b
   DevParams d;
   rc = to_dev(params, &d);
   if (rc) return rc;
+  if (sh.gen_fwd)
+    return nais_gx_forward(params, hist, b, n, hist_ld, target, hist_region, hist_region_ld,
+                           target_region, target_lat_long, latlon_ld, out, nan_count, flags, st);
   NAIS_DISPATCH(launch_forward, sh.DH, sh.HB, params->variant, d, hist, b, n, hist_ld, target,
                 hist_region, hist_region_ld, target_region, target_lat_long, latlon_ld, out,
                 nan_count, flags, st);
@@ -3030,7 +3043,10 @@ int32_t nais_score_topk(const nais_params_t* params, const int64_t* indptr, cons
   const int64_t ld = round_up(params->num_pois, 64);
   for (int32_t u0 = 0; u0 < num_users; u0 += MAX_BATCH_USERS) {
     const int nb = std::min<int32_t>(MAX_BATCH_USERS, num_users - u0);
-    if (params->precision == NAIS_PRECISION_FP16X6)
+    if (sh.gen_cat)
+      rc = nais_gx_catalog(params, indptr, indices, users + u0, nb, nullptr, 0, 0, 0, region_of,
+                           coords, latlon_mat, scores, ld, nan_count, nullptr, nullptr, 0, st);
+    else if (params->precision == NAIS_PRECISION_FP16X6)
       NAIS_DISPATCH(launch_catalog_x6b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
                     nb, region_of, coords, latlon_mat, scores, ld, nan_count, st);
     else if (params->precision == NAIS_PRECISION_FP16X6_PAIRSPLIT)
@@ -3094,6 +3110,9 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
   DevParams d;
   rc = to_dev(params, &d);
   if (rc) return rc;
+  if (sh.gen_tab)
+    return nais_gx_catalog(params, nullptr, nullptr, nullptr, 0, items, num_items, col0, cols,
+                           region_of, coords, latlon_mat, nullptr, 0, nullptr, e, es, ld, st);
   TableOut tab;
   tab.ld = ld;
   tab.cols = cols;
@@ -3155,7 +3174,11 @@ int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,
   if (rc) return rc;
   for (int32_t u0 = 0; u0 < num_users; u0 += 65535) {
     const int nb = std::min<int32_t>(65535, num_users - u0);
-    if (params->precision == NAIS_PRECISION_FP16X6)
+    if (sh.gen_cat)
+      rc = nais_gx_catalog(params, indptr, indices, users + u0, nb, nullptr, 0, 0, 0, region_of,
+                           coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld, nan_count,
+                           nullptr, nullptr, 0, st);
+    else if (params->precision == NAIS_PRECISION_FP16X6)
       NAIS_DISPATCH(launch_catalog_x6b, sh.DH, sh.HB, params->variant, d, indptr, indices, users + u0,
                     nb, region_of, coords, latlon_mat, scores + (int64_t)u0 * score_ld, score_ld,
                     nan_count, st);

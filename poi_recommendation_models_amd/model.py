@@ -145,12 +145,11 @@ class _NAISDevice(nn.Module):
         when a parameter changes (tensor version counter). Training reads the parameters as they
         are (the training kernels take any D, H <= 128)."""
         D = int(self.embed_size)
-        if D in NATIVE_WIDTHS:
+        if D in NATIVE_WIDTHS or D > NATIVE_WIDTHS[-1]:
+            # above 128 the library's generic-shape kernels (nais_generic.hip, exact fp32) take the
+            # parameters as they are, up to embed_size 256 (NAIS_E_UNSUPPORTED beyond)
             return self.nais_params()
-        Dp = next((w for w in NATIVE_WIDTHS if w >= D), None)
-        if Dp is None:
-            raise RuntimeError(f"embed_size {D} > 128: the scoring kernels hold a 128-wide embedding "
-                               "tile at most (LDS / VGPR budget)")
+        Dp = next(w for w in NATIVE_WIDTHS if w >= D)
         region = self.VARIANT in (_capi.VARIANT_REGION, _capi.VARIANT_REGION_DISTANCE)
         dist = self.VARIANT in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE)
         eh, et = self._item_tables()
