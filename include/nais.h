@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 11   /* 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
+#define NAIS_ABI_VERSION 12   /* 12: any embed_dim <= 256 and any hidden (generic-shape kernels); 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -69,12 +69,16 @@ extern "C" {
 
 /*
  * Parameters of one NAIS model: device pointers to the reference's nn.Module parameters
- * (state_dict names in comments) plus their dimensions. The scoring entry points are compiled for
- * embed_dim in {8, 16, 32, 64, 128}; a caller with another width <= 128 zero-pads the tables (each
- * half of the region variants' rows separately) and attn_layer1's columns to the next of those
- * (exact; the Python drop-in does this, model._NAISDevice._score_params). hidden: 1..256 -- above
- * 128 for precision FP16X6 at embed_dim 32, 64, 128 and for nais_forward (NAIS_E_UNSUPPORTED
- * otherwise); the training entry points take any embed_dim and hidden up to 128.
+ * (state_dict names in comments) plus their dimensions. Shapes (the reference builds
+ * Linear(embed_size, hidden_size) for any sizes, model.py:9-38): embed_dim 1..256, hidden >= 1,
+ * every entry point. The tuned kernels are compiled for embed_dim in {8, 16, 32, 64, 128} and
+ * hidden <= 256 (scoring at precision FP16X6 with embed_dim 32 / 64 / 128, and nais_forward;
+ * <= 128 for the other catalog precisions); every other shape runs the generic-shape kernels
+ * (exact fp32 whatever the precision; nais_generic.hip) -- a caller with a width < 128 off that
+ * set may instead zero-pad the tables (each half of the region variants' rows separately) and
+ * attn_layer1's columns to the next native width for the tuned kernels (exact; the Python drop-in
+ * does, model._NAISDevice._score_params). Training: the tuned / general kernels up to 128, the
+ * generic-shape ones above. embed_dim > 256 is NAIS_E_UNSUPPORTED (the LDS budget).
  */
 typedef struct nais_params {
   int32_t variant;              /* NAIS_VARIANT_* */
@@ -435,8 +439,9 @@ int32_t nais_pair_distances(const double* coords, const int64_t* hist, int64_t n
  * the reference repeats it b times, batches.py:30). Replaces, for this batch shape,
  *   prediction = model(user_history, train_data)   (run.py:103; model.py:40-89 in train mode)
  *   loss.backward()                                (run.py:105; BCELoss model.py:21)
- * NAIS_VARIANT_BASIC; embed_dim / hidden up to 128 (fused MFMA kernels at embed_dim in {8,16,32,64},
- * hidden <= 64; a general kernel otherwise -- see nais_train_forward_ex for the region variants).
+ * NAIS_VARIANT_BASIC; embed_dim up to 256, any hidden (fused MFMA kernels at embed_dim in
+ * {8,16,32,64}, hidden <= 64; a general kernel up to 128; the generic-shape kernels above -- see
+ * nais_train_forward_ex for the region variants).
  *
  * Dropout (nn.Dropout(dropout_p), model.py:22,71) keeps hidden unit i of pair (row c, item j) iff
  * a counter hash of (seed, c*n + j, i) is >= dropout_p * 2^32 and scales kept units by 1/(1-p);

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4

@@ -140,6 +140,36 @@ __device__ __forceinline__ void block_logits(const Shape& s, const float* __rest
   if (TWO) pb += qb;
 }
 
+// z = b1 + W1 x of one staged hidden block for one target row t against the 32 items of Lh (C
+// layout: lane (n, hh) holds hidden rows crow(0, r, hh) of item n) -- the training backward's
+// recompute of the forward (block_logits' arithmetic, one chain)
+template <bool DIST>
+__device__ __forceinline__ floatx16 block_z(const Shape& s, const float* __restrict__ Lw,
+                                            const float* __restrict__ Lbw, const float* __restrict__ Lh,
+                                            const float* __restrict__ t, const float* __restrict__ f,
+                                            int lane) {
+  const int n = lane & 31, hh = lane >> 5;
+  floatx16 A;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) A[r] = Lbw[crow(0, r, hh)];
+  const float* hrow = Lh + n * s.HP;
+  const float* wrow = Lw + n * s.Q;
+  const int D2 = s.D & ~1;
+#pragma unroll 4
+  for (int k0 = 0; k0 < D2; k0 += 2) {
+    const int k = k0 + hh;
+    A = mfma(wrow[k], hrow[k] * t[k], A);
+  }
+  for (int k0 = D2; k0 < s.DINP; k0 += 2) {
+    const int k = k0 + hh;
+    float x = 0.f;
+    if (k < s.D) x = hrow[k] * t[k];
+    else if (DIST && k < s.DIN) x = f[2 * n + (k - s.D)];
+    A = mfma(wrow[k], x, A);
+  }
+  return A;
+}
+
 struct NoDrop {
   __device__ __forceinline__ float operator()(uint32_t, int) const { return 1.f; }
 };

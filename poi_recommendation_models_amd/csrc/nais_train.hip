@@ -38,6 +38,7 @@
 
 #include "nais.h"
 #include "nais_internal.h"
+#include "nais_gx.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
@@ -1413,6 +1414,343 @@ gm_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __rest
   TFLUSH();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Generic-shape training kernels (nais_gx.h): embed_dim in (128, 256] or hidden above 128 -- the
+// shapes the general kernels above cannot hold (their whole W1 in LDS, hidden <= 128 in
+// accumulators). Same math, dropout hash, partials and gradient outputs as gm_forward_kernel /
+// gm_backward_kernel; one W1 hidden block at a time in LDS. A unit is (4 * tpw rows, one 32-item
+// slice of the shared history); wave w takes rows w * tpw .. w * tpw + tpw - 1, two at a time in
+// the forward MFMAs.
+//   forward:  per (slice, row) S = sum e, N = sum e (h . t)  (gm_forward_kernel's Sp / Np)
+//   backward: pass 1 recomputes the logits (every hidden block) -> e, ds, da per pair; pass 2 per
+//             hidden block: z again -> du (ReLU / dropout backward), db1 / dw2 (reduce-scatter
+//             into LDS), du^T staged in the wave's LDS rows, dx = W1_blk^T du per 32-dim block
+//             consumed at once into the history-row grads (LDS atomics per item) and the target
+//             rows (wave-owned LDS rows), the distance features' grads (dims D, D + 1 of dx),
+//             and the dW1 tiles (A = du^T, B = x, over the row's 32 pairs) in registers across
+//             the wave's rows, added to the gradient once per (wave, hidden block).
+// ---------------------------------------------------------------------------------------------
+constexpr int GXT_MAX_TPW = 8;
+constexpr int GXT_MAX_DBX = (gx::GX_MAX_D + 2 + 31) / 32;   // dW1 column tiles (din <= 258)
+
+struct GxTL {
+  int o_w, o_bw, o_h, o_t, o_f, o_l, o_id, o_gh, o_gt, o_du, o_db, o_dw, o_df, o_gd, o_da, fwd, bwd;
+  __host__ __device__ GxTL(const gx::Shape& s, int rt) {
+    auto al = [](int x) { return (x + 3) & ~3; };
+    o_w = 0;
+    o_bw = al(32 * s.Q);
+    o_h = o_bw + 64;
+    o_t = al(o_h + 32 * s.HP);
+    o_f = al(o_t + rt * s.D);       // [rt][32][2] distance features f0, f1 of the row's pairs
+    o_l = o_f + rt * 64;            // [rt][32][2] their scaled inputs (100 |dlat|, 100 |dlng|)
+    o_id = o_l + rt * 64;           // [32] int64 item ids
+    fwd = o_id + 64;
+    o_gh = fwd;                     // [32][HP] history-row grads of the slice
+    o_gt = al(o_gh + 32 * s.HP);    // [rt][D]  target-row grads
+    o_du = al(o_gt + rt * s.D);     // [rt][32 pairs][33] du^T of the current hidden block
+    o_db = o_du + rt * 32 * 33;     // [HB * 32] db1
+    o_dw = o_db + s.HB * 32;        // [HB * 32] dw2
+    o_df = o_dw + s.HB * 32;        // [rt][32][2] d(feature) of the row's pairs
+    o_gd = o_df + rt * 64;          // [8] dist_layer weight / bias grads
+    o_da = o_gd + 8;                // [rt][32][2] ds, da of the row's pairs (pass 1 -> pass 2)
+    bwd = o_da + rt * 64;
+  }
+};
+
+// the unit's operands: the slice's full history rows and ids, the rows' full target rows and the
+// pairs' distance features
+__device__ __forceinline__ void gxt_stage(const GArgs& a, const gx::Shape& s, const GxTL& o, float* L,
+                                          int tid, int64_t c0, int rt, int64_t j0, int nj) {
+  for (int f = tid; f < 32 * s.D; f += gx::GX_NT) {
+    const int jj = f / s.D, d = f % s.D;
+    L[o.o_h + jj * s.HP + d] = jj < nj ? hfull(a, j0 + jj, d) : 0.f;
+  }
+  if (tid < 32) reinterpret_cast<int64_t*>(L + o.o_id)[tid] = tid < nj ? a.hist[j0 + tid] : -1;
+  for (int f = tid; f < rt * s.D; f += gx::GX_NT) {
+    const int rq = f / s.D, d = f % s.D;
+    const int64_t c = c0 + rq;
+    L[o.o_t + f] = c < a.b ? tfull(a, c, d) : 0.f;
+  }
+  if (s.DIN > s.D) {
+    for (int f = tid; f < rt * 32; f += gx::GX_NT) {
+      const int rq = f >> 5, jj = f & 31;
+      const int64_t c = c0 + rq;
+      float f0 = 0.f, f1 = 0.f, l0 = 0.f, l1 = 0.f;
+      if (c < a.b && jj < nj) {
+        const float* ll = a.ll + c * a.ll_ld + 2 * (j0 + jj);
+        l0 = ll[0] * a.dscale;
+        l1 = ll[1] * a.dscale;
+        // sigmoid(dist_layer(100 ll)), model.py:265, in the scorer's operation order
+        f0 = 1.0f / (1.0f + expf(-(l0 * a.dw[0] + l1 * a.dw[1] + a.db[0])));
+        f1 = 1.0f / (1.0f + expf(-(l0 * a.dw[2] + l1 * a.dw[3] + a.db[1])));
+      }
+      L[o.o_f + 2 * f] = f0;
+      L[o.o_f + 2 * f + 1] = f1;
+      L[o.o_l + 2 * f] = l0;
+      L[o.o_l + 2 * f + 1] = l1;
+    }
+  }
+}
+
+struct GxDrop {
+  Drop d;
+  __device__ __forceinline__ float operator()(uint32_t k, int i) const { return d.factor(k, i); }
+};
+
+// pass 1 of both kernels: the attention logit and h . t of the wave's rows' 32 pairs
+template <bool DIST, bool DROP>
+__device__ __forceinline__ void gxt_logits(const GArgs& a, const gx::Shape& s, const GxTL& o, float* L,
+                                           int tid, int lane, int w, int tpw, int64_t c0, int64_t j0,
+                                           float (&pa)[GXT_MAX_TPW], float (&sd)[GXT_MAX_TPW]) {
+  const int n = lane & 31;
+  const GxDrop drop{a.drop};
+#pragma unroll
+  for (int t = 0; t < GXT_MAX_TPW; ++t) pa[t] = sd[t] = 0.f;
+  for (int hb = 0; hb < s.HB; ++hb) {
+    __syncthreads();
+    gx::stage_w1_block(a.w1, a.b1, a.w2, s, hb, L + o.o_w, L + o.o_bw, tid, gx::GX_NT);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < GXT_MAX_TPW / 2; ++q) {
+      if (2 * q >= tpw) continue;
+      const int ra = w * tpw + 2 * q;
+      const uint32_t ka = DROP ? a.drop.key(uint32_t((c0 + ra) * a.n + j0 + n)) : 0u;
+      const uint32_t kb = DROP ? a.drop.key(uint32_t((c0 + ra + 1) * a.n + j0 + n)) : 0u;
+      gx::block_logits<true, DIST, DROP>(s, L + o.o_w, L + o.o_bw, L + o.o_h, L + o.o_t + ra * s.D,
+                                         L + o.o_t + (ra + 1) * s.D, L + o.o_f + ra * 64,
+                                         L + o.o_f + (ra + 1) * 64, lane, hb, hb == 0, pa[2 * q],
+                                         pa[2 * q + 1], sd[2 * q], sd[2 * q + 1], drop, ka, kb);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < GXT_MAX_TPW; ++t) {
+    pa[t] += __shfl_xor(pa[t], 32);
+    sd[t] += __shfl_xor(sd[t], 32);
+  }
+}
+
+template <bool DIST>
+__global__ void __launch_bounds__(gx::GX_NT, 1)
+gxt_forward_kernel(GArgs a, float* __restrict__ Sp, float* __restrict__ Np, int tpw) {
+  extern __shared__ float4 glds4[];
+  float* L = reinterpret_cast<float*>(glds4);
+  const gx::Shape s(a.D, a.DIN, a.H);
+  const int rt = 4 * tpw;
+  const GxTL o(s, rt);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31;
+  const int64_t nrt = (a.b + rt - 1) / rt;
+  const int64_t sl = blockIdx.x / nrt, c0 = (blockIdx.x % nrt) * rt, j0 = sl * 32;
+  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+  gxt_stage(a, s, o, L, tid, c0, rt, j0, nj);
+  float pa[GXT_MAX_TPW], sd[GXT_MAX_TPW];
+  if (a.drop.on) gxt_logits<DIST, true>(a, s, o, L, tid, lane, w, tpw, c0, j0, pa, sd);
+  else gxt_logits<DIST, false>(a, s, o, L, tid, lane, w, tpw, c0, j0, pa, sd);
+  const int64_t item = reinterpret_cast<const int64_t*>(L + o.o_id)[n];
+#pragma unroll
+  for (int t = 0; t < GXT_MAX_TPW; ++t) {
+    const int64_t c = c0 + w * tpw + t;
+    if (t >= tpw || c >= a.b) continue;
+    const float e = n < nj ? expf(pa[t]) * (item != a.target[c] ? 1.f : 0.f) : 0.f;   // model.py:74-78
+    const float S = half_sum(e), N = half_sum(e * sd[t]);
+    if (lane == 0) {
+      Sp[sl * a.b + c] = S;
+      Np[sl * a.b + c] = N;
+    }
+  }
+}
+
+template <bool DIST>
+__global__ void __launch_bounds__(gx::GX_NT, 1)
+gxt_backward_kernel(GArgs a, const float* __restrict__ saved, const float* __restrict__ pred,
+                    const float* __restrict__ gpred, GGrads gr, const int32_t* __restrict__ bad_rows,
+                    int tpw) {
+  if (bad_rows && *bad_rows) return;   // fused step on a NaN batch: no update (see train_loss)
+  extern __shared__ float4 glds4[];
+  float* L = reinterpret_cast<float*>(glds4);
+  const gx::Shape s(a.D, a.DIN, a.H);
+  const int rt = 4 * tpw;
+  const GxTL o(s, rt);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 31, hh = lane >> 5;
+  const int64_t nrt = (a.b + rt - 1) / rt;
+  const int64_t sl = blockIdx.x / nrt, c0 = (blockIdx.x % nrt) * rt, j0 = sl * 32;
+  const int nj = (int)(a.n - j0 < 32 ? a.n - j0 : 32);
+  gxt_stage(a, s, o, L, tid, c0, rt, j0, nj);
+  for (int f = tid; f < o.bwd - o.o_gh; f += gx::GX_NT) L[o.o_gh + f] = 0.f;
+  // ---- pass 1: logits -> e, ds, da per pair (gm_backward_kernel's formulas)
+  float pa[GXT_MAX_TPW], sd[GXT_MAX_TPW];
+  if (a.drop.on) gxt_logits<DIST, true>(a, s, o, L, tid, lane, w, tpw, c0, j0, pa, sd);
+  else gxt_logits<DIST, false>(a, s, o, L, tid, lane, w, tpw, c0, j0, pa, sd);
+  const int64_t item = reinterpret_cast<const int64_t*>(L + o.o_id)[n];
+#pragma unroll
+  for (int t = 0; t < GXT_MAX_TPW; ++t) {
+    float ds = 0.f, da = 0.f;
+    const int64_t c = c0 + w * tpw + t;
+    if (t < tpw && c < a.b) {
+      const float e = n < nj ? expf(pa[t]) * (item != a.target[c] ? 1.f : 0.f) : 0.f;
+      const float S = saved[c], N = saved[a.b + c], pc = pred[c];
+      const float gl = gpred[c] * pc * (1.f - pc);                // dL/dlogit (sigmoid)
+      const float Sb = (a.beta == 0.5f) ? sqrtf(S) : powf(S, a.beta);
+      ds = gl / Sb * e;                                             // dlogit / ds_cj
+      da = ds * (sd[t] - a.beta * N / S);                           // dlogit / da_cj
+    }
+    if (t < tpw && lane < 32) {   // both lane halves hold the pair's values
+      L[o.o_da + (w * tpw + t) * 64 + 2 * n] = ds;
+      L[o.o_da + (w * tpw + t) * 64 + 2 * n + 1] = da;
+    }
+  }
+  // ---- pass 2, per hidden block. Phase A per row: z again -> du (kept in the wave's LDS rows as
+  // du^T), db1 / dw2, dx per 32-dim block consumed into the history / target-row grads and the
+  // distance features' grads. Phase B per 32-column block of W1: the dW1 tile over every row of
+  // the wave (A = du^T, B = x), added to the gradient once per (wave, hidden block, column block).
+  const float kscale = a.drop.on ? a.drop.scale : 1.f;
+  const int DB = (s.D + 31) / 32, DBX = (s.DIN + 31) / 32;
+  for (int hb = 0; hb < s.HB; ++hb) {
+    __syncthreads();
+    gx::stage_w1_block(a.w1, a.b1, a.w2, s, hb, L + o.o_w, L + o.o_bw, tid, gx::GX_NT);
+    __syncthreads();
+    const float* Lw = L + o.o_w;
+    const float* Lbw = L + o.o_bw;
+#pragma unroll 1
+    for (int t = 0; t < tpw; ++t) {
+      const int rq = w * tpw + t;
+      const int64_t c = c0 + rq;
+      float* Ldu = L + o.o_du + rq * 32 * 33;
+      if (c >= a.b) {   // a row past the batch: du = 0 for phase B
+        for (int f = lane; f < 32 * 33; f += 64) Ldu[f] = 0.f;
+        continue;
+      }
+      const float dsp = L[o.o_da + rq * 64 + 2 * n], dap = L[o.o_da + rq * 64 + 2 * n + 1];
+      const float* trow = L + o.o_t + rq * s.D;
+      floatx16 z = gx::block_z<DIST>(s, Lw, Lbw, L + o.o_h, trow, L + o.o_f + rq * 64, lane);
+      const uint32_t key = a.drop.on ? a.drop.key(uint32_t(c * a.n + j0 + n)) : 0u;
+      float vb[16], vz[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = gx::crow(0, r, hh);
+        float v = z[r];
+        if (a.drop.on) v *= a.drop.factor(key, 32 * hb + i);
+        // ReLU + dropout backward: v > 0 only where the unit was kept (gm_backward_kernel)
+        const float du = v > 0.f ? dap * Lbw[32 + i] * kscale : 0.f;
+        z[r] = du;
+        vb[r] = du;
+        vz[r] = dap * nais_relu(v);
+        Ldu[n * 33 + i] = du;                                       // du^T: [pair][hidden]
+      }
+      const float tb = half_reduce_scatter<16>(vb, lane);
+      const float tz = half_reduce_scatter<16>(vz, lane);
+      if ((n & 1) == 0) {
+        const int i = gx::crow(0, n >> 1, hh);
+        atomicAdd(&L[o.o_db + 32 * hb + i], tb);
+        atomicAdd(&L[o.o_dw + 32 * hb + i], tz);
+      }
+      const bool live = n < nj;
+#pragma unroll 1
+      for (int q = 0; q < DBX; ++q) {
+        // dx rows 32 q .. 32 q + 31 (dims; past D: the distance features' d(feature))
+        floatx16 dx;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dx[r] = 0.f;
+        const int col = (32 * q + n) < s.Q ? 32 * q + n : 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dx = gx::mfma(Lw[gx::crow(0, r, hh) * s.Q + col], z[r], dx);
+        float vt[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = 32 * q + gx::crow(0, r, hh);
+          vt[r] = 0.f;
+          if (d < s.D && live) {
+            const float rv = dx[r] + (hb == 0 ? dsp : 0.f);
+            atomicAdd(&L[o.o_gh + n * s.HP + d], rv * trow[d]);
+            vt[r] = rv * L[o.o_h + n * s.HP + d];
+          } else if (DIST && d >= s.D && d < s.DIN && live) {
+            L[o.o_df + rq * 64 + 2 * n + (d - s.D)] += dx[r];       // wave-owned row, one lane
+          }
+        }
+        if (q < DB) {
+          const float tt = half_reduce_scatter<16>(vt, lane);
+          const int d = 32 * q + gx::crow(0, n >> 1, hh);
+          if ((n & 1) == 0 && d < s.D) L[o.o_gt + rq * s.D + d] += tt;   // wave-owned row
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // phase B: the wave's dW1 tiles of this hidden block
+#pragma unroll 1
+    for (int q = 0; q < DBX; ++q) {
+      floatx16 gw;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gw[r] = 0.f;
+      const int k = 32 * q + n;
+#pragma unroll 1
+      for (int t = 0; t < tpw; ++t) {
+        const int rq = w * tpw + t;
+        const float* Ldu = L + o.o_du + rq * 32 * 33;
+        const float tk = k < s.D ? L[o.o_t + rq * s.D + k] : 0.f;
+#pragma unroll 4
+        for (int t2 = 0; t2 < 16; ++t2) {
+          const int p = 2 * t2 + hh;
+          float x = 0.f;
+          if (k < s.D) x = L[o.o_h + p * s.HP + k] * tk;
+          else if (DIST && k < s.DIN) x = L[o.o_f + rq * 64 + 2 * p + (k - s.D)];
+          gw = gx::mfma(Ldu[p * 33 + n], x, gw);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = 32 * hb + gx::crow(0, r, hh);
+        if (i < s.H && k < s.DIN) unsafeAtomicAdd(&gr.w1[int64_t(i) * s.DIN + k], gw[r]);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- the unit's flush: history rows, target rows, db1 / dw2, dist_layer
+  for (int f = tid; f < nj * s.D; f += gx::GX_NT) {
+    const int jj = f / s.D, d = f % s.D;
+    const int64_t j = j0 + jj;
+    const float v = L[o.o_gh + jj * s.HP + d];
+    if (d < a.IDIM) unsafeAtomicAdd(&gr.eh[a.hist[j] * a.IDIM + d], v);
+    else unsafeAtomicAdd(&gr.er[a.hreg[j] * a.RDIM + (d - a.IDIM)], v);
+  }
+  for (int f = tid; f < rt * s.D; f += gx::GX_NT) {
+    const int rq = f / s.D, d = f % s.D;
+    const int64_t c = c0 + rq;
+    if (c >= a.b) continue;
+    const float v = L[o.o_gt + f];
+    if (d < a.IDIM) unsafeAtomicAdd(&gr.et[a.target[c] * a.IDIM + d], v);
+    else unsafeAtomicAdd(&gr.er[a.treg[c] * a.RDIM + (d - a.IDIM)], v);
+  }
+  for (int i = tid; i < s.H; i += gx::GX_NT) {
+    unsafeAtomicAdd(&gr.b1[i], L[o.o_db + i]);
+    unsafeAtomicAdd(&gr.w2[i], L[o.o_dw + i]);
+  }
+  if (DIST) {   // sigmoid, then dist_layer (Linear(2, 2)), summed over the unit's pairs
+    float qv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int f = tid; f < rt * 32; f += gx::GX_NT) {
+      const int rq = f >> 5, jj = f & 31;
+      if (c0 + rq >= a.b || jj >= nj) continue;
+      const float f0 = L[o.o_f + 2 * f], f1 = L[o.o_f + 2 * f + 1];
+      const float q0 = L[o.o_df + 2 * f] * f0 * (1.f - f0), q1 = L[o.o_df + 2 * f + 1] * f1 * (1.f - f1);
+      const float l0 = L[o.o_l + 2 * f], l1 = L[o.o_l + 2 * f + 1];
+      qv[0] += q0 * l0;
+      qv[1] += q0 * l1;
+      qv[2] += q1 * l0;
+      qv[3] += q1 * l1;
+      qv[4] += q0;
+      qv[5] += q1;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      float v = qv[k];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) atomicAdd(&L[o.o_gd + k], v);
+    }
+    __syncthreads();
+    if (tid < 6) unsafeAtomicAdd(tid < 4 ? &gr.dw[tid] : &gr.db[tid - 4], L[o.o_gd + tid]);
+  }
+}
+
 size_t g_lds_bytes(const GArgs& a, bool backward, int gw = GW) {
   const GL g(a.D, a.H, a.DIN, gw);
   return size_t(backward ? g.bwd : g.fwd) * sizeof(float);
@@ -1527,6 +1865,9 @@ int hip_rc(hipError_t e, const char* what) {
 }
 
 // the fused MFMA kernels cover NAIS_basic at D in {8, 16, 32, 64}, H <= 64
+// the generic-shape training kernels' shapes (no u cache there: the backward recomputes z)
+bool gx_shape(const nais_params_t* p) { return p->embed_dim > G_MAX_D || p->hidden > G_MAX_H; }
+
 bool fast_ok(const nais_params_t* p) {
   const int D = p->embed_dim;
   return p->variant == NAIS_VARIANT_BASIC && (D == 8 || D == 16 || D == 32 || D == 64) &&
@@ -1538,8 +1879,9 @@ int gvalidate(const nais_params_t* p, const nais_train_side_t* side, int64_t b, 
   if (!p->embed_history || !p->embed_target || !p->w1 || !p->b1 || !p->w2)
     return nais_internal_fail(NAIS_E_INVALID, "missing parameter pointer");
   const int D = p->embed_dim;
-  if (D <= 0 || D > G_MAX_D || p->hidden <= 0 || p->hidden > G_MAX_H)
-    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: embed_dim and hidden must be in [1, 128]");
+  // up to 128 the general kernels, above (embed_dim <= 256, any hidden) the generic-shape ones
+  if (D <= 0 || D > gx::GX_MAX_D || p->hidden <= 0)
+    return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: embed_dim must be in [1, 256], hidden >= 1");
   switch (p->variant) {
     case NAIS_VARIANT_BASIC:
       if (p->item_dim != D || p->din != D)
@@ -1631,6 +1973,51 @@ int device_cus() {
 // the backward at D = 128 with the 2 distance inputs spills (256 VGPRs + 36): runtime-shaped there
 #define NAIS_GM_SHAPES_BWD(X) X(4, 128, 128, 0) X(2, 64, 64, 0) X(2, 64, 64, 2)
 
+// rows per wave of the generic training kernels: the most of 8 / 4 / 2 whose LDS image fits
+int gxt_tpw(const GArgs& a, bool backward) {
+  const gx::Shape s(a.D, a.DIN, a.H);
+  for (int tpw = GXT_MAX_TPW; tpw >= 2; tpw /= 2) {
+    const GxTL o(s, 4 * tpw);
+    if (size_t(backward ? o.bwd : o.fwd) * 4 <= 160 * 1024) return tpw;
+  }
+  return 0;
+}
+
+bool gxt_big(const GArgs& a) { return a.D > G_MAX_D || a.H > G_MAX_H; }
+
+int gxt_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
+  const int tpw = gxt_tpw(a, false);
+  if (!tpw) return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: shape exceeds the generic kernels' LDS budget");
+  const gx::Shape s(a.D, a.DIN, a.H);
+  const size_t lds = size_t(GxTL(s, 4 * tpw).fwd) * 4;
+  static bool once = (set_lds(gxt_forward_kernel<false>, 160 * 1024), set_lds(gxt_forward_kernel<true>, 160 * 1024), true);
+  (void)once;
+  const int64_t units = ((a.b + 4 * tpw - 1) / (4 * tpw)) * ((a.n + 31) / 32);
+  if (a.DIN > a.D)
+    hipLaunchKernelGGL(gxt_forward_kernel<true>, dim3((unsigned)units), dim3(gx::GX_NT), lds, st, a, Sp, Np, tpw);
+  else
+    hipLaunchKernelGGL(gxt_forward_kernel<false>, dim3((unsigned)units), dim3(gx::GX_NT), lds, st, a, Sp, Np, tpw);
+  return nais_internal_check_launch("gxt_forward_kernel");
+}
+
+int gxt_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
+                 const GGrads& g, hipStream_t st, const int32_t* bad_rows) {
+  const int tpw = gxt_tpw(a, true);
+  if (!tpw) return nais_internal_fail(NAIS_E_UNSUPPORTED, "training: shape exceeds the generic kernels' LDS budget");
+  const gx::Shape s(a.D, a.DIN, a.H);
+  const size_t lds = size_t(GxTL(s, 4 * tpw).bwd) * 4;
+  static bool once = (set_lds(gxt_backward_kernel<false>, 160 * 1024), set_lds(gxt_backward_kernel<true>, 160 * 1024), true);
+  (void)once;
+  const int64_t units = ((a.b + 4 * tpw - 1) / (4 * tpw)) * ((a.n + 31) / 32);
+  if (a.DIN > a.D)
+    hipLaunchKernelGGL(gxt_backward_kernel<true>, dim3((unsigned)units), dim3(gx::GX_NT), lds, st, a, saved, pred,
+                       gpred, g, bad_rows, tpw);
+  else
+    hipLaunchKernelGGL(gxt_backward_kernel<false>, dim3((unsigned)units), dim3(gx::GX_NT), lds, st, a, saved, pred,
+                       gpred, g, bad_rows, tpw);
+  return nais_internal_check_launch("gxt_backward_kernel");
+}
+
 template <int GWT>
 int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64_t units, int sl0,
                      int trows = 0) {
@@ -1689,6 +2076,7 @@ int64_t g_split_slices(const GArgs& a) {
 // one per workgroup's last round instead of a full-length third round on 85 of them.
 // NAIS_GM_FWD_TAIL=0: twelve-row short units (A/B).
 int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
+  if (gxt_big(a)) return gxt_forward(a, Sp, Np, st);
   const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
   static const bool fwd_tail = [] {
     const char* e = getenv("NAIS_GM_FWD_TAIL");
@@ -1728,6 +2116,7 @@ int g_backward_launch(const GArgs& a, const float* saved, const float* pred, con
 
 int g_backward(const GArgs& a, const float* saved, const float* pred, const float* gpred,
                const GGrads& g, hipStream_t st, const int32_t* bad_rows = nullptr) {
+  if (gxt_big(a)) return gxt_backward(a, saved, pred, gpred, g, st, bad_rows);
   const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
   const int64_t first = GM_BWD_PERSIST ? nsl : g_split_slices(a);
   int rc = g_backward_launch<GW>(a, saved, pred, gpred, g, st, bad_rows, nrt * first, 0);
@@ -1743,14 +2132,14 @@ extern "C" {
 namespace {
 // the caller's u cache of the autograd split (nais_train_side_t::ucache), when large enough
 float* side_ucache(const nais_params_t* params, const nais_train_side_t* side, int64_t b, int64_t n) {
-  if (!side || !side->ucache || fast_ok(params) || b <= 0 || n <= 0) return nullptr;
+  if (!side || !side->ucache || fast_ok(params) || gx_shape(params) || b <= 0 || n <= 0) return nullptr;
   const size_t need = ucache_bytes(params->hidden, b, n);
   return (need <= UCACHE_MAX_BYTES && side->ucache_bytes >= need) ? side->ucache : nullptr;
 }
 
 // the fused step's u cache (general kernels only), after saved / gpred / pred / the partials
 size_t step_ucache_bytes(const nais_params_t* params, int64_t b, int64_t n) {
-  if (!params || b <= 0 || n <= 0 || fast_ok(params)) return 0;
+  if (!params || b <= 0 || n <= 0 || fast_ok(params) || gx_shape(params)) return 0;
   const size_t u = ucache_bytes(params->hidden, b, n);
   return u <= UCACHE_MAX_BYTES ? u : 0;
 }
@@ -1761,7 +2150,7 @@ size_t step_ucache_offset(const nais_params_t* params, int64_t b, int64_t n) {
 }  // namespace
 
 size_t nais_train_ucache_size(const nais_params_t* params, int64_t b, int64_t n) {
-  if (!params || b <= 0 || n <= 0 || fast_ok(params)) return 0;
+  if (!params || b <= 0 || n <= 0 || fast_ok(params) || gx_shape(params)) return 0;
   const size_t u = ucache_bytes(params->hidden, b, n);
   return u <= UCACHE_MAX_BYTES ? u : 0;
 }

@@ -51,15 +51,19 @@ def test_validation_errors_without_device(lib):
     rc = lib.nais_forward(None, None, 1, 1, 1, None, None, 0, None, None, 0, None, None, 1, None)
     assert rc == -1 and b"params" in lib.nais_last_error()
     p = _capi.NaisParams()
-    p.variant, p.embed_dim, p.item_dim, p.din, p.hidden, p.num_pois = 0, 12, 12, 12, 16, 10
+    p.variant, p.embed_dim, p.item_dim, p.din, p.hidden, p.num_pois = 0, 264, 264, 264, 16, 10
     for f in ("embed_history", "embed_target", "w1", "b1", "w2"):
         setattr(p, f, 16)
     rc = lib.nais_forward(p, 16, 1, 1, 1, 16, None, 0, None, None, 0, 16, None, 1, None)
-    assert rc == -2 and b"multiple of 8" in lib.nais_last_error()
-    p.embed_dim = p.item_dim = p.din = 16
-    p.hidden = 300                       # the kernels take hidden <= 256 (ABI 11)
+    assert rc == -2 and b"256" in lib.nais_last_error()   # any embed_dim <= 256 (ABI 12)
+    p.variant, p.embed_dim, p.item_dim, p.din = 1, 12, 5, 12        # region: item_dim == embed_dim/2
     rc = lib.nais_forward(p, 16, 1, 1, 1, 16, None, 0, None, None, 0, 16, None, 1, None)
-    assert rc == -2 and b"256" in lib.nais_last_error()
+    assert rc == -1 and b"region" in lib.nais_last_error()
+    p.variant = 0
+    p.embed_dim = p.item_dim = p.din = 16
+    p.hidden = 0
+    rc = lib.nais_forward(p, 16, 1, 1, 1, 16, None, 0, None, None, 0, 16, None, 1, None)
+    assert rc == -2 and b"hidden" in lib.nais_last_error()
     p.hidden = 16
     assert lib.nais_score_topk(p, 16, 16, 16, 1, 2000, None, None, None, None, 16, 16, None, None,
                                16, 1 << 30, None) == -2

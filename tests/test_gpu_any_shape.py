@@ -248,3 +248,38 @@ def test_padded_copies_follow_native_optimizer_writes(writer):
     after = check("after " + writer)
     moved = max(float(np.max(np.abs(after[k] - before[k]))) for k in before)
     assert moved > 1e-3                       # the parameters did change
+
+
+@pytest.mark.parametrize("D,H,drop", [(192, 192, 0.5), (64, 320, 0.0), (256, 96, 0.5)])
+def test_fused_step_big_shapes_vs_oracle(D, H, drop):
+    """run.py:91-109 (the fused NAISTrainer step: forward, BCELoss, backward, Adagrad) at embed /
+    hidden sizes past the general kernels (the generic-shape training kernels), two steps of a
+    config-3-like batch (204 positives x 5) against the float64 oracle, dropout mask injected."""
+    from test_gpu_train import _batch, _csr, _mask, _params, _trainer
+    from test_gpu_train import _model as _train_model
+    from _helpers import adagrad_slack, assert_params_close
+    P, n = 3000, 204
+    p = _params(P, D, H, seed=D + H)
+    m = _train_model(p, drop_p=drop)
+    tr = _trainer(m, _csr(2, P, 10, seed=4), lr=0.02)
+    ref = {k: v.copy() for k, v in p.items()}
+    st = {k: np.zeros_like(v) for k, v in p.items()}
+    slack = {k: np.zeros(v.shape) for k, v in p.items()}
+    first_g, total = {}, 0.0
+    for step in (1, 2):
+        hist, data, labels = _batch(P, n, 4, seed=60 + step)
+        seed = 5150 + step
+        tr.step(torch.as_tensor(hist).to(DEV), torch.as_tensor(data).to(DEV),
+                torch.as_tensor(labels).to(DEV), dropout_seed=seed)
+        loss = tr.finish() - total
+        total += loss
+        keep = _mask(seed, len(data), n, H, drop) if drop else None
+        r = train_oracle.train_step_basic(ref, hist, data, labels, keep=keep, drop_p=drop)
+        assert abs(loss - r["loss"]) <= 1e-5, (step, loss, r["loss"])
+        for k in ref:
+            g = r["grads"][k].reshape(ref[k].shape)
+            slack[k] += adagrad_slack(g, 0.02)
+            first_g.setdefault(k, g)
+            ref[k], st[k] = train_oracle.adagrad(ref[k], st[k], g, 0.02, step)
+    for k, q in m.named_parameters():
+        assert_params_close(k, q.detach().cpu().numpy(), ref[k], slack[k], g=first_g[k])
