@@ -30,11 +30,15 @@ def hipcc():
 OBJDIR = os.path.join(ROOT, "build_obj")   # per-translation-unit object cache (git- and gpurun-ignored)
 
 
-def build(force=False, extra=(), out=None, extra_for=None):
+def build(force=False, extra=(), out=None, extra_for=None, replace=None):
     """Compile the kernels into OUT (or `out`, e.g. an A/B variant with extra -D flags). Objects are
     cached per (translation unit, flags) under build_obj/: a TU is recompiled only when it or a
     header is newer than its object, so an edit to one .hip file (or an A/B -D flag that one TU
-    reads, passed through `extra_for` = {basename: flags}) recompiles that file alone."""
+    reads, passed through `extra_for` = {basename: flags}) recompiles that file alone. `replace` =
+    {basename: path} compiles another source in that TU's place (a probe build that includes the
+    product source, e.g. scripts/probes/train_timing.hip) -- never for the product library."""
+    if replace and out is None:
+        raise ValueError("replace= builds a variant: give it out=")
     import hashlib
     OUT_ = out or OUT
     csrc = os.path.join(HERE, "csrc")
@@ -49,11 +53,17 @@ def build(force=False, extra=(), out=None, extra_for=None):
     os.makedirs(OBJDIR, exist_ok=True)
     objs, todo = [], []
     for src in SRCS:
-        f = [*flags, *PER_SRC.get(os.path.basename(src), ()), *(extra_for or {}).get(os.path.basename(src), ())]
+        base = os.path.basename(src)
+        f = [*flags, *PER_SRC.get(base, ()), *(extra_for or {}).get(base, ())]
+        newest = max(os.path.getmtime(src), hdr_time)
+        if replace and base in replace:
+            src = os.path.abspath(replace[base])
+            f = [*f, "-DNAIS_PROBE_SOURCE=" + os.path.basename(src)]
+            newest = max(newest, os.path.getmtime(src))
         key = hashlib.sha1(" ".join(f).encode()).hexdigest()[:12]
-        o = os.path.join(OBJDIR, f"{os.path.basename(src)}.{key}.o")
+        o = os.path.join(OBJDIR, f"{base}.{key}.o")
         objs.append(o)
-        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr_time):
+        if force or not os.path.exists(o) or os.path.getmtime(o) < newest:
             todo.append((src, o, f))
     # the link is keyed too: a sidecar next to the library records the objects it was linked
     # from (their names carry the flag hashes), so a variant name reused with other -D flags, or

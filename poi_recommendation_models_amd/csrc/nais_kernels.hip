@@ -1467,9 +1467,7 @@ struct X6Slices {
 // With the cheaper feature (v_exp / v_rcp, the folded exponent) group 3 wins at D = 64: table block
 // 2.093 / 2.075 / 2.077 ms and the config-4 job 0.616 / 0.614 / 0.612 s at groups 1 / 0 / 3
 // (profiles/r5/fa); D = 128 keeps group 1 (unmeasured since).
-#ifndef NAIS_X6N_FEATS_AT
-#define NAIS_X6N_FEATS_AT -1   // -1: 3 at D <= 64, 1 at D = 128
-#endif
+constexpr int X6N_FEATS_AT = -1;   // -1: 3 at D <= 64, 1 at D = 128
 // The distance term as two v_mfma_f32_16x16x1_4b_f32 per PAIR of 16-hidden blocks (the four 16x16
 // tiles (m, nb) of the pair as the instruction's four blocks, K = 1 feature each; layout probed,
 // scripts/probes/mfma_4b_layout.hip, profiles/r5/d4b) instead of two v_mfma_f32_16x16x4_f32 per
@@ -1488,16 +1486,12 @@ __device__ __forceinline__ floatx16 mfma4b(float a, float b, floatx16 c) {
 // 437 VALU per 4-item block at D = 64) 1.983 -> 1.998 ms at D = H = 64, 7.198 -> 7.228 ms at 128
 // (profiles/r5/pk): the block is not issue-bound.
 
-#ifndef NAIS_X6N_EPI_PREFETCH
-#define NAIS_X6N_EPI_PREFETCH 1
-#endif
-#ifndef NAIS_X6N_EPI_REGS
-#define NAIS_X6N_EPI_REGS 1
-#endif
-#ifndef NAIS_X6N_W1_VGPRS
-#define NAIS_X6N_W1_VGPRS 32   // W1 values a thread may hold in VGPRs (more: W1G). 16 (W1 from L2
-                               // at D = H = 128 too): 20 -> 23 spilled VGPRs there, so not that
-#endif
+// (the A/B switches of the round-5 x6n work are constants since round 6: EPI_PREFETCH and EPI_REGS
+// are described, with their measurements, where they are used below)
+constexpr bool X6N_EPI_PREFETCH = true;
+constexpr bool X6N_EPI_REGS = true;
+constexpr int X6N_W1_VGPRS = 32;   // W1 values a thread may hold in VGPRs (more: W1G). 16 (W1 from L2
+                                   // at D = H = 128 too): 20 -> 23 spilled VGPRs there, so not that
 template <int D, int MB, int NHU, bool DIST = false>
 struct CfgN {
   static constexpr int KS = D / 32;                    // K-steps of 32 dims
@@ -1525,7 +1519,7 @@ struct CfgN {
   static constexpr int GQ = (NHU / GU) > 2 ? NHU / GU : 2;
   // W1 read from global memory (L2) at each build instead of held in VGPRs when a thread's
   // share of it would take more than 32 VGPRs (D = 128 with more than 128 hidden units)
-  static constexpr bool W1G = NHU * EPT * 8 > NAIS_X6N_W1_VGPRS;
+  static constexpr bool W1G = NHU * EPT * 8 > X6N_W1_VGPRS;
   static_assert(BYTES <= 160 * 1024, "x6n: LDS");
   static_assert((GQ * GU) % NHU == 0 && GQ % 2 == 0 && GQ <= 4, "x6n: a round of groups spans whole items");
 };
@@ -1805,7 +1799,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // (profiles/r5/er). (D = 128 would spill; the distance variants sit at 245 VGPRs already.) The
   // tail's s / history-id reads and the build's history-row reads a group ahead as well: neutral
   // (block 1.863 vs 1.855 / 1.858 ms without either, job 0.5964 / 0.5958 / 0.5961 s, profiles/r5/tp).
-  constexpr bool ER = NAIS_X6N_EPI_REGS && NHU == 1 && !DIST && D <= 64;
+  constexpr bool ER = X6N_EPI_REGS && NHU == 1 && !DIST && D <= 64;
   float4 breg[ER ? MB : 1], wreg[ER ? MB : 1];
   auto wld = [&](const float* ewb, int m) __attribute__((always_inline)) {
     if constexpr (ER) return wreg[m];
@@ -1843,7 +1837,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // reads, so the wait for them is a counted one that leaves the A reads in flight (where ER does
     // not apply; lgkmcnt(0) waits per hot block 22 -> 13 at D = H = 128: block 7.478 -> 7.404 ms,
     // region_distance 2.200 -> 2.180 ms, its config-4 job 0.620 -> 0.617 s, profiles/r5/ep)
-    constexpr bool EP = !ER && NAIS_X6N_EPI_PREFETCH;
+    constexpr bool EP = !ER && X6N_EPI_PREFETCH;
     float4 bnx = {0.f, 0.f, 0.f, 0.f}, wnx = {0.f, 0.f, 0.f, 0.f};
     auto eload = [&](int g) __attribute__((always_inline)) {   // what group g's consumers need
       const int m = g / KS, s = g % KS;
@@ -1902,13 +1896,13 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
           }
         }
         // a unit of the next group, at the step's middle group (D = H = 128 block 7.60 -> 7.45 ms
-        // against the last group; D = 64 unchanged -- profiles/r4/ab6)
-#ifndef NAIS_X6N_PROBE_NOBUILD   // timing probe only (wrong results): the in-step build's cost
+        // against the last group; D = 64 unchanged -- profiles/r4/ab6). (Round 5 timed the kernel
+        // without this build, wrong results: 1.822 of 2.050 ms per D = 64 table block, MFMA busy
+        // 0.64 instead of 0.56, profiles/r5/pmc_probe; the probe switch is gone since round 6.)
         if (g == NG / 2) build(bu, std::integral_constant<int, HB>{}, bgrp, bit);
-#endif
         // the next item's distance features, in the item's last unit (compile-time)
         if constexpr (DIST && HC == NHU - 1)
-          if (g == std::min(NAIS_X6N_FEATS_AT >= 0 ? NAIS_X6N_FEATS_AT : (D <= 64 ? 3 : 1), NG - 1))
+          if (g == std::min(X6N_FEATS_AT >= 0 ? X6N_FEATS_AT : (D <= 64 ? 3 : 1), NG - 1))
             feats(NHU == 1 ? cur + 1 : cur / NHU + 1);
       }
       if constexpr (D == 128) {
@@ -2050,9 +2044,9 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
       };
       one(std::integral_constant<int, 0>{});
       if constexpr (GU == 2) one(std::integral_constant<int, 1>{});
-#ifndef NAIS_X6N_PROBE_NOBAR   // timing probe only (wrong results): the group barrier's cost
+      // (without this barrier, a round-5 timing probe with racing ring slots: 1.998 vs 2.050 ms
+      // per D = 64 table block, profiles/r5/pmc_probe)
       __syncthreads();
-#endif
     };
     for (int g = 0; g < ngroups; g += C::GQ) {
       group(g, std::integral_constant<int, 0>{});

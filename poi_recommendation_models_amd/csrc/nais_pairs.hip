@@ -131,10 +131,7 @@ constexpr int STRIPE = 64 * CPL;             // columns per wave
 // count does not unroll here (the loop holds convergent readlanes), which left one row -- 2 KB per
 // wave -- in flight and the gather latency-bound; GU explicit loads per step keep GU rows in flight
 // while the adds stay in history (CSR) order.
-#ifndef NAIS_PAIR_GU
-#define NAIS_PAIR_GU 8   // config-4 job at 4 / 8 / 12 / 16 rows: 0.607 / 0.597 / 0.606 / 0.657 s (profiles/r5/gu)
-#endif
-constexpr int GU = NAIS_PAIR_GU;
+constexpr int GU = 8;   // config-4 job at 4 / 8 / 12 / 16 rows: 0.607 / 0.597 / 0.606 / 0.657 s (profiles/r5/gu)
 
 // CPL columns of one table row for a lane with nv valid columns (CPL: one vector load; fewer, the
 // last lane of a block whose width is not a multiple of CPL: scalar loads, 0 past the block).

@@ -49,26 +49,11 @@ constexpr int TTHREADS = TW * 64;
 constexpr int TROWS = TW * 32;      // batch rows per workgroup: 32 per wave (the MFMA columns)
 constexpr int MAX_JS = 32;          // history items per slice (grid.y)
 
-// Optional per-phase cycle accounting of the backward kernel (A/B builds only:
-// -DNAIS_TRAIN_TIMING=1 adds nais_debug_train_cycles(); scripts/train_phases.py reads it).
-#ifndef NAIS_TRAIN_TIMING
-#define NAIS_TRAIN_TIMING 0
-#endif
-#if NAIS_TRAIN_TIMING
-__device__ unsigned long long g_train_cycles[16];
-#define TSTART() unsigned long long t_prev = __builtin_amdgcn_s_memtime(), t_acc[16] = {0}
-#define TMARK(k)                                            \
-  do {                                                      \
-    const unsigned long long t_now = __builtin_amdgcn_s_memtime(); \
-    t_acc[k] += t_now - t_prev;                             \
-    t_prev = t_now;                                         \
-  } while (0)
-#define TFLUSH()                                                             \
-  do {                                                                       \
-    if ((threadIdx.x & 63) == 0)                                             \
-      for (int q = 0; q < 16; ++q) atomicAdd(&g_train_cycles[q], t_acc[q]);  \
-  } while (0)
-#else
+// Per-phase cycle accounting hooks of the backward kernels: no-ops in the product library. The
+// timing build (scripts/probes/train_timing.hip) defines them -- s_memtime deltas per phase, summed
+// into a device array that its nais_debug_train_cycles() reads (scripts/train_phases.py) -- and
+// includes this file; the hooks never change a result.
+#ifndef TSTART
 #define TSTART() (void)0
 #define TMARK(k) (void)0
 #define TFLUSH() (void)0
@@ -859,10 +844,8 @@ make_batch_kernel(const int64_t* __restrict__ indptr, const int64_t* __restrict_
 // and adds them to the caller's gradients with global atomics; target-row grads go straight from
 // registers.
 // ---------------------------------------------------------------------------------------------
-#ifndef NAIS_GM_GW
-#define NAIS_GM_GW 12   // 3 waves per SIMD (153-167 VGPRs); A/B vs 8: step 0.567 -> 0.530 ms at D = H = 128
-#endif
-constexpr int GW = NAIS_GM_GW;        // rows (waves) per workgroup
+constexpr int GW = 12;   // rows (waves) per workgroup: 3 waves per SIMD (153-167 VGPRs); A/B vs 8:
+                         // step 0.567 -> 0.530 ms at D = H = 128
 constexpr int G_MAX_D = 128, G_MAX_H = 128, G_MAX_DIN = G_MAX_D + 2;
 
 struct GArgs {
@@ -901,27 +884,22 @@ size_t ucache_bytes(int H, int64_t b, int64_t n) {
   return size_t(units * GW * int64_t(((H + 31) / 32) * 16 + 2) * 64) * sizeof(float);
 }
 constexpr size_t UCACHE_MAX_BYTES = size_t(1) << 30;   // above: the backward recomputes u
-#ifndef NAIS_UCACHE_NT
-#define NAIS_UCACHE_NT 1   // non-temporal u-cache stores / loads (A/B vs 0: 0.512 vs 0.516 ms per step)
-#endif
+constexpr bool UCACHE_NT = true;   // non-temporal u-cache stores / loads (A/B vs default: 0.512 vs 0.516 ms per step)
 __device__ __forceinline__ void uc_store(float v, float* p) {
-  if (NAIS_UCACHE_NT) __builtin_nontemporal_store(v, p);
+  if (UCACHE_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 __device__ __forceinline__ float uc_load(const float* p) {
-  if (NAIS_UCACHE_NT) return __builtin_nontemporal_load(p);
+  if (UCACHE_NT) return __builtin_nontemporal_load(p);
   return *p;
 }
 
 // The backward's global atomics at config 3, D = H = 128 (timing-only builds without them,
 // profiles/r5/train_bwd/r5diag): dW1 0.033 ms, history-row grads 0.022 ms of the 0.427 ms.
 
-// The general backward runs one unit per workgroup (persistent = 1 keeps W1 staged across units but
-// spills at D = H = 128: the A/B knob).
-#ifndef NAIS_GM_BWD_PERSIST
-#define NAIS_GM_BWD_PERSIST 0
-#endif
-constexpr bool GM_BWD_PERSIST = NAIS_GM_BWD_PERSIST;
+// The general backward runs one unit per workgroup (a persistent form keeping W1 staged across
+// units spills at D = H = 128; its code path stays for the shapes that may use it).
+constexpr bool GM_BWD_PERSIST = false;
 
 // The LDS base as an opaque per-iteration value: inside the persistent unit loops, reads of the
 // loop-invariant W1 image would otherwise be hoisted out of the loop into (spilled) registers.
@@ -2046,22 +2024,20 @@ int g_forward_launch(const GArgs& a, float* Sp, float* Np, hipStream_t st, int64
   return nais_internal_check_launch("gm_forward_kernel");
 }
 
-#ifndef NAIS_GM_TAIL
-#define NAIS_GM_TAIL 4   // rows per workgroup of the short-slice launches; 0 = one launch each
+constexpr int GM_TAIL = 4;   // rows per workgroup of the short-slice launches; 0 = one launch each
 // (config-3 step at D = H = 128, interleaved: 4 rows 0.487 / 0.485 ms, 2 rows 0.558 / 0.566, 6 rows
 // 0.497 / 0.497, 8 rows 0.498 / 0.497 -- profiles/r5/train_tail)
-#endif
 // The general kernels' units are (row tile, 32-item slice) workgroups, one per CU (LDS). When the
 // short last slice (n % 32 items) pushes the unit count into one more round of workgroups over the
 // CUs -- config 3: 85 row tiles x 7 slices = 595 units = 2.3 rounds of 256, the third almost empty
 // but as long as a full one, since a slice of 12 items costs the MFMAs of 32 -- that slice runs as
-// a second launch of NAIS_GM_TAIL-row workgroups (one wave per SIMD, a third of a unit's waves)
+// a second launch of GM_TAIL-row workgroups (one wave per SIMD, a third of a unit's waves)
 // after the full slices' exactly-filled rounds (the backward; see g_forward). Returns the number of
 // full slices to launch first (== the slice count when no split pays).
 int64_t g_split_slices(const GArgs& a) {
   const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32, nfull = a.n / 32;
   const int64_t cus = device_cus();
-  if (NAIS_GM_TAIL <= 0 || nfull == 0 || nsl == nfull) return nsl;
+  if (GM_TAIL <= 0 || nfull == 0 || nsl == nfull) return nsl;
   const char* off = getenv("NAIS_GM_TAIL");   // "0": one launch (tests compare both forms)
   if (off && off[0] == '0' && off[1] == 0) return nsl;
   const int64_t rounds_all = (nrt * nsl + cus - 1) / cus, rounds_full = (nrt * nfull + cus - 1) / cus;
@@ -2071,7 +2047,7 @@ int64_t g_split_slices(const GArgs& a) {
 // The forward stays one persistent launch: its workgroups stage W1 once for all their units, so
 // the short slice's units ride on workgroups that already hold it (A/B, config 3 at D = H = 128:
 // split 0.129 ms vs 0.110 ms -- a 4-row tail workgroup pays a whole W1 staging for one unit).
-// Inside that launch the short slice's units are NAIS_GM_TAIL-row tiles when the backward splits
+// Inside that launch the short slice's units are GM_TAIL-row tiles when the backward splits
 // (same criterion, g_split_slices): config 3's 85 twelve-row short units become 255 four-row ones,
 // one per workgroup's last round instead of a full-length third round on 85 of them.
 // NAIS_GM_FWD_TAIL=0: twelve-row short units (A/B).
@@ -2082,7 +2058,7 @@ int g_forward(const GArgs& a, float* Sp, float* Np, hipStream_t st) {
     const char* e = getenv("NAIS_GM_FWD_TAIL");
     return !(e && e[0] == '0');
   }();
-  const int trows = (fwd_tail && NAIS_GM_TAIL > 0 && g_split_slices(a) < nsl) ? NAIS_GM_TAIL : 0;
+  const int trows = (fwd_tail && GM_TAIL > 0 && g_split_slices(a) < nsl) ? GM_TAIL : 0;
   const int64_t units = trows > 0 ? nrt * (nsl - 1) + (a.b + trows - 1) / trows : nrt * nsl;
   return g_forward_launch<GW>(a, Sp, Np, st, units, 0, trows);
 }
@@ -2120,8 +2096,8 @@ int g_backward(const GArgs& a, const float* saved, const float* pred, const floa
   const int64_t nrt = (a.b + GW - 1) / GW, nsl = (a.n + 31) / 32;
   const int64_t first = GM_BWD_PERSIST ? nsl : g_split_slices(a);
   int rc = g_backward_launch<GW>(a, saved, pred, gpred, g, st, bad_rows, nrt * first, 0);
-  if (rc || first == nsl || NAIS_GM_TAIL <= 0) return rc;
-  constexpr int TW_ = NAIS_GM_TAIL > 0 ? NAIS_GM_TAIL : 1;
+  if (rc || first == nsl || GM_TAIL <= 0) return rc;
+  constexpr int TW_ = GM_TAIL > 0 ? GM_TAIL : 1;
   return g_backward_launch<TW_>(a, saved, pred, gpred, g, st, bad_rows, (a.b + TW_ - 1) / TW_, (int)first);
 }
 
@@ -2548,17 +2524,5 @@ int32_t nais_adagrad_rows(float* param, float* state_sum, const float* grad, int
   return nais_internal_check_launch("adagrad_rows_kernel");
 }
 
-#if NAIS_TRAIN_TIMING
-int32_t nais_debug_train_cycles(unsigned long long* out16, int32_t reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_train_cycles), 16 * sizeof(unsigned long long)) !=
-      hipSuccess)
-    return NAIS_E_HIP;
-  if (reset) {
-    static const unsigned long long z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_train_cycles), z, sizeof(z)) != hipSuccess) return NAIS_E_HIP;
-  }
-  return NAIS_OK;
-}
-#endif
 
 }  // extern "C"

@@ -1,7 +1,8 @@
 """Build A/B variants of libnais_hip.so with extra -D flags into build_ab/<name>.so (CPU side;
 the .so files travel to the GPU box). Usage: python scripts/build_ab.py name=-DFOO=1,-DBAR=2 ...
 or name=nais_train.hip:-DFOO=1 to give the flags to that translation unit only (the others reuse
-the cached objects of the default build)."""
+the cached objects of the default build), or name=nais_train.hip@scripts/probes/train_timing.hip
+to compile a probe source (which includes the product file) in that unit's place."""
 import os
 import sys
 
@@ -13,6 +14,10 @@ os.makedirs(out_dir, exist_ok=True)
 for spec in sys.argv[1:]:
     name, _, flags = spec.partition("=")
     tu = None
+    if "@" in flags:
+        tu, _, probe = flags.partition("@")
+        print(b.build(replace={tu: probe}, out=os.path.join(out_dir, name + ".so")), tu, probe, flush=True)
+        continue
     if ":" in flags:
         tu, _, flags = flags.partition(":")
     extra = [f for f in flags.split(",") if f]

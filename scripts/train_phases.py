@@ -1,5 +1,6 @@
-"""Per-phase cycle split of the training backward kernel (A/B build with -DNAIS_TRAIN_TIMING=1).
-  NAIS_HIP_LIB=.../libnais_timing.so python scripts/train_phases.py [--D 64 --H 64 --n 204]
+"""Per-phase cycle split of the training backward kernel (the timing build scripts/probes/train_timing.hip:
+  python scripts/build_ab.py timing=nais_train.hip@scripts/probes/train_timing.hip).
+  NAIS_HIP_LIB=build_ab/timing.so python scripts/train_phases.py [--D 64 --H 64 --n 204]
 Phases (s_memtime deltas summed over waves): 0 prologue, 1 u recompute + exp, 2 du/db1/dw2 + LDS
 writes, 3 dx MFMA + dt, 4 dh reduce-scatter, 5 barrier, 6 dW1 MFMA, 7 barrier, 8 flush.
 --fused: the trainer's fused step (NAISTrainer.step, u cache on) instead of the forward + backward
