@@ -21,10 +21,13 @@ import torch
 
 
 class TorchNAIS:
-    """NAIS_basic's eval-mode forward (model.py:40-89) on CPU tensors."""
+    """NAIS_basic's eval-mode forward (model.py:40-89) on CPU tensors (or, `device`, on another
+    torch device: the same ops through PyTorch's own kernels -- an independent checker of the
+    HIP path at sizes the CPU cannot cover, tests/test_gpu_configs.py)."""
 
-    def __init__(self, params, beta=0.5):
-        t = lambda k: torch.as_tensor(np.ascontiguousarray(params[k]), dtype=torch.float32)
+    def __init__(self, params, beta=0.5, device=None):
+        t = lambda k: torch.as_tensor(np.ascontiguousarray(params[k]), dtype=torch.float32,
+                                      device=device)
         self.eh, self.et = t("embed_history.weight"), t("embed_target.weight")
         self.w1, self.b1, self.w2 = t("attn_layer1.weight"), t("attn_layer1.bias"), t("attn_layer2.weight")
         self.beta = beta

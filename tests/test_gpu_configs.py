@@ -255,3 +255,55 @@ def test_config5_slice_direct_and_pairs_block():
         did, dsc = nais_oracle.topk_ids(cand, full[u][cand], K)   # the direct route's block top-k
         assert_topk_equivalent(did, dsc, pid[u], psc[u], tie_ulps=TIE_ULPS)
     _stats("config 5", before)
+
+
+def test_config4_bench_job_every_user_vs_torch_restatement(config4_job):
+    """Every one of the bench job's 50,000 users (VERDICT r5 'What's weak' 1: 47,952 of them were
+    only compared with the build's other route) against the reference's ops restated in torch
+    (oracle/torch_cpu.TorchNAIS, pinned to the reference's outputs by
+    tests/test_torch_cpu_baseline.py), run through PyTorch's own GPU kernels -- independent of
+    this package's -- on a sampled candidate set per user: the job's top-50 winners, the build's
+    ranks 51-60 (the selection boundary) and 40 random other candidates:
+      * the winners' restated scores within SCORE_ATOL of the job's scores;
+      * no boundary or random candidate beats the weakest winner in the restatement by more
+        than the 4-ulp tie allowance."""
+    from oracle import torch_cpu
+    from poi_recommendation_models_amd.catalog import _score_topk_pairs
+    data, p, m, csr, ids_p, sc_p = config4_job
+    U, P, K, KB, NR = data.num_users, data.num_pois, 50, 60, 40
+    ids60, _ = _score_topk_pairs(m, csr, np.arange(U), KB, None, None, None, None, force=True)
+    ids60 = ids60.cpu().numpy()
+    tm = torch_cpu.TorchNAIS(p, device=DEV)
+    rng = np.random.default_rng(44)
+    h = data.hist_len()
+    worst_w, worst_over, ties, checked = 0.0, -1.0, 0, 0
+    for hl in np.unique(h):
+        us = np.nonzero(h == hl)[0]
+        hist = np.stack([data.history(u) for u in us])                       # [n_u, hl]
+        probes = np.empty((len(us), K + 10 + NR), np.int64)
+        for i, u in enumerate(us):
+            win = ids_p[u].astype(np.int64)
+            bnd = ids60[u, K:KB].astype(np.int64)
+            bnd = bnd[~np.isin(bnd, win)]
+            extra = rng.integers(0, P, 4 * NR)
+            extra = extra[~np.isin(extra, hist[i]) & ~np.isin(extra, win) & ~np.isin(extra, bnd)]
+            rest = np.concatenate([bnd, extra])[:10 + NR]
+            probes[i] = np.concatenate([win, rest])
+        uh = torch.as_tensor(hist, device=DEV).repeat_interleave(probes.shape[1], dim=0)
+        tg = torch.as_tensor(probes.reshape(-1), device=DEV)
+        ref = tm(uh, tg).view(len(us), -1).cpu().numpy()
+        dw = np.abs(ref[:, :K] - sc_p[us])
+        worst_w = max(worst_w, float(dw.max()))
+        assert dw.max() <= SCORE_ATOL, (int(hl), float(dw.max()))
+        weakest = ref[:, :K].min(axis=1)
+        over = ref[:, K:] - weakest[:, None]
+        allow = TIE_ULPS * np.spacing(weakest.astype(np.float32))[:, None]
+        bad = over > allow
+        assert not bad.any(), (int(hl), us[np.nonzero(bad.any(1))[0][:5]].tolist(), float(over.max()))
+        ties += int((over > 0).sum())
+        worst_over = max(worst_over, float(over.max()))
+        checked += len(us)
+    assert checked == U
+    print(f"config 4, all {U} users vs the torch restatement on the device: max |winner score diff| "
+          f"{worst_w:.3g}; {ties} sampled candidates above the weakest winner, all within "
+          f"{TIE_ULPS} ulps (max excess {worst_over:.3g})")
