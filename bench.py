@@ -825,8 +825,11 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     entries = int(hist_len.sum())
     J = int(np.count_nonzero(np.bincount(data.indices, minlength=P)))
     fused = catalog.PAIR_FUSED_TOPK and K <= 256
-    Wb, st_w = catalog.PAIR_BLOCK_COLS, catalog.PAIR_STRIPE
-    stripes = sum((min(Wb, NC - b) + st_w - 1) // st_w for b in range(0, NC, Wb))
+    Wb = catalog.PAIR_BLOCK_COLS
+
+    def stripes_of(bounded):
+        st_w = catalog.PAIR_BOUNDED_STRIPE if bounded else catalog.PAIR_STRIPE
+        return sum((min(Wb, NC - b) + st_w - 1) // st_w for b in range(0, NC, Wb)), st_w
     flop_per_pair_item = 2 * D * H + 3 * H + 4 * D
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
 
@@ -835,10 +838,14 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         (`flop_item`: algorithmic FLOP per (pair, history item) when not NAIS_basic's; `steps`:
         the leg's timed steps when not a_steps[precision])."""
         ns = steps or a_steps[precision]
-        # table rows (8 B per history entry x column) + each stripe's CSR ids and row map (12 B
-        # per entry) + score rows (4 B per user x column; the fused kernel writes only the top-k
-        # merges); with PAIR_TABLE_GATHER_FRAC > 0 only the gather stream's share is timed
-        gbytes = entries * NC * 8 + entries * 12 * stripes + (0 if fused else a.num_users * NC * 4)
+        bounded = bool(per.get("bounded"))
+        stripes, st_w = stripes_of(bounded)
+        # table rows (8 B per history entry x column; the bounded gather: 4 B, the hi words) + each
+        # stripe's CSR ids and row map (12 B per entry) + score rows (4 B per user x column; the
+        # fused kernels write only the top-k merges); with PAIR_TABLE_GATHER_FRAC > 0 only the
+        # gather stream's share is timed
+        gbytes = (entries * NC * (4 if bounded else 8) + entries * 12 * stripes
+                  + (0 if fused else a.num_users * NC * 4))
         gbytes *= per.get("gather_share", 1.0)
         g_ms = sum(per.get("gather", [])) / ns
         t_ms = sum(per.get("table", [])) / ns
@@ -849,18 +856,27 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
         t_ach = tflops / (t_ms * 1e-3) / 1e12 if t_ms else None
         gcus = ncu - table_cus if table_cus < ncu else ncu
         gather = {
-            "kernel": "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
-                      "pair_gather_kernel (nais_pair_gather)",
+            "kernel": ("pair_bound_topk_kernel (nais_pair_bound_topk)" if bounded else
+                       "pair_gather_topk_kernel (nais_pair_gather_topk)" if fused else
+                       "pair_gather_kernel (nais_pair_gather)"),
             "bound": "hbm", "achieved": g_ach, "peak": HBM_SPEC_GBS, "unit": "GB/s",
             "frac": g_ach / HBM_SPEC_GBS if g_ach else None,
             "frac_of_measured_hbm": g_ach / HBM_MEASURED_GBS if g_ach else None,
             "measured_hbm_peak": HBM_MEASURED_GBS,
-            "served_from": ("Infinity Cache (MALL) mostly: the 256-column stripe of the tables "
-                            "(J x 256 x 8 B ~ 205 MB) fits the 256 MB MALL, so the memory side "
-                            "delivers more than the HBM copy rate"),
+            "served_from": ("Infinity Cache (MALL) mostly: the %d-column stripe of the tables "
+                            "(J x %d x %d B ~ %.0f MB) fits the 256 MB MALL, so the memory side "
+                            "delivers more than the HBM copy rate"
+                            % (st_w, st_w, 4 if bounded else 8, J * st_w * (4 if bounded else 8) / 1e6)),
             "algorithmic_bytes_per_launch": gbytes / n_gl, "avg_launch_ms": g_ms / n_gl,
             "launches_per_step": n_gl, "ms_per_step": g_ms, "cus": gcus,
         }
+        if bounded:
+            gather["refine_ms_per_step"] = sum(per.get("refine", [])) / ns
+            gather["route"] = ("bounded: split16 tables, the gather streams the hi words (e, e*s "
+                               "truncated to 8 significant bits) and keeps per user the k best lower "
+                               "bounds + the candidates whose upper bound reaches them; the refine "
+                               "recomputes those exactly from hi + lo in CSR order (the exact "
+                               "gather's bits, exact_gather_path.identical)")
         table = {
             "kernel": (kname or table_kernel_name(precision, D, H)) + " in table mode (nais_pair_table)",
             "bound": "mfma", "achieved": t_ach, "peak": PEAKS[precision], "unit": "TFLOP/s",
@@ -896,8 +912,8 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     if "traffic" not in dominant:
         dominant["traffic"] = None
     dominant["note"] = ("gather: algorithmic bytes per launch (one %d-column stripe) = sum_u h_u x "
-                        "columns x 8 B table reads + 12 B CSR id + row map per history entry; table: "
-                        % st_w +
+                        "columns x %d B table reads + 12 B CSR id + row map per history entry; table: "
+                        % (stripes_of(bool(per.get("bounded")))[1], 4 if per.get("bounded") else 8) +
                         "SURVEY.md 8(d) FLOP per (pair, history item) x distinct history POIs x "
                         "columns; traffic = rocprofv3 (2 x FETCH_SIZE + WRITE_SIZE) per launch")
     dominant["overlap"] = ("tables on CUs [0, %d) and gathers on the other %d, side by side on "
@@ -906,6 +922,28 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     dominant["other_kernel"] = other
     dominant["topk_ms_per_step"] = k_ms
     legs = {}
+    if world == 1 and per.get("bounded"):
+        # the same job on the exact fused gather (float tables, 8 B per history entry and column):
+        # its time, and the headline's lists against it -- the same ids and score bits
+        catalog.PAIR_BOUNDED = False
+        try:
+            el_x, per_x = run(a.precision, 1, a.leg_steps)
+        finally:
+            catalog.PAIR_BOUNDED = True
+        g_x, t_x = kernels(per_x, a.precision, steps=a.leg_steps)
+        xi, xs = (t.cpu().numpy() for t in last["out"])
+        hi_, hs_ = (t.cpu().numpy() for t in head_out)
+        st = getattr(model, "_last_bound_stats", None)
+        st = st.cpu().numpy() if st is not None else None
+        legs["exact_gather"] = {
+            "what": "the exact fused gather (pair_gather_topk_kernel on float e / e*s tables) on the "
+                    "same job",
+            "value": pairs_job * a.leg_steps / el_x, "unit": "pairs/s", "steps": a.leg_steps,
+            "ms_per_step": el_x / a.leg_steps * 1e3, "gather": g_x, "table_ms_per_step": t_x["ms_per_step"],
+            "identical": bool(np.array_equal(xi, hi_) and np.array_equal(xs.view(np.uint32), hs_.view(np.uint32))),
+            "users": int(xi.shape[0]),
+            "bounded_refined_per_user": None if st is None else float(st[0]) / max(1, a.num_users),
+            "bounded_overflowed_users": None if st is None else int(st[1])}
     if world == 1 and not a.no_fp32_leg:
         for prec in ("fp32", "fp16x3"):
             if prec == a.precision:
@@ -1039,6 +1077,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "roofline": dominant,
             "cpu_baseline": cpu,
             "self_check": check,
+            "exact_gather_path": legs.get("exact_gather"),
             "fp32_path": legs.get("fp32"),
             "fp16x3_path": legs.get("fp16x3"),
             "prior_path": legs.get("prior"),

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 12   /* 12: any embed_dim <= 256 and any hidden (generic-shape kernels); 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
+#define NAIS_ABI_VERSION 13   /* 13: split16 pair tables, bounded gather + exact refine (nais_pair_table_split, nais_pair_bound_topk, nais_pair_refine_topk); 12: any embed_dim <= 256 and any hidden (generic-shape kernels); 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -262,6 +262,45 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
                               void* stream);
 int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32_t num_users, int32_t k,
                               int32_t* out_ids, float* out_scores, int32_t* short_count, void* stream);
+/*
+ * Bounded gather + exact refine (filter-and-refine top-k; DESIGN.md (d) "bounded gather"): the
+ * lists of nais_pair_gather_topk -- the same ids and score bits -- from half the gathered bytes.
+ *   nais_pair_table_split  nais_pair_table's pairs stored split16: hi[r*ld + c-col0] = (top 16 bits
+ *                      of e*s) << 16 | (top 16 bits of e), lo[...] = the low 16 bits likewise; hi
+ *                      alone holds both values truncated to 8 significant bits, hi + lo the fp32 bits.
+ *   nais_pair_bound_topk   per column block (stream-ordered over the blocks of one user list): each
+ *                      user's S, N = sum over its history of the truncated e, e*s and sum |e*s| give
+ *                      an interval around every candidate's exact score (the fp32 arithmetic of
+ *                      nais_pair_gather_topk on the untruncated pairs); lo_keys[slot*k ..] / lo_count
+ *                      keep the k best lower bounds (zero lo_count before the first block), and the
+ *                      key (upper bound, id) of every candidate whose upper bound reaches the k-th
+ *                      lower bound so far is appended to surv[slot*surv_cap ..] (surv_count[slot];
+ *                      zero it before the first block; compacted when full, -1 if it overflows).
+ *                      Keys as nais_pair_gather_topk. ld % 4 == 0, hi 16-byte aligned, k <= 256.
+ *   nais_pair_refine_topk  after the last block: for each survivor whose upper key reaches the final
+ *                      k-th lower key (every column for an overflowed user), the exact N, S from
+ *                      hi + lo in history (CSR) order and its score; keys / kcount receive the top-k
+ *                      exactly as nais_pair_gather_topk leaves them (NaNs counted into *nan_count).
+ *                      Tables: block b (columns col0 + b*block_cols ..) has hi at tables +
+ *                      b*block_stride and lo lo_offset elements further, row pitch ld. stats (may be
+ *                      NULL): stats[0] += candidates refined, stats[1] += overflowed users.
+ */
+int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                              int64_t col0, int64_t cols, const int64_t* region_of,
+                              const double* coords, const double* latlon_mat, uint32_t* hi,
+                              uint32_t* lo, int64_t ld, int32_t* work, void* stream);
+int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowmap,
+                             const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                             int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                             uint64_t* lo_keys, int32_t* lo_count, uint64_t* surv, int32_t* surv_count,
+                             int32_t surv_cap, int32_t* work, void* stream);
+int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int64_t lo_offset,
+                              int64_t ld, int64_t block_cols, const int32_t* rowmap,
+                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                              const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
+                              const int32_t* surv_count, int32_t surv_cap, uint64_t* keys,
+                              int32_t* kcount, int32_t* nan_count, int32_t* stats, void* stream);
 /*
  * Power-law prior on the pairs route (powerLaw.py:86-92, run.py:537-539; the direct route's
  * nais_score_topk with a prior computes the same G rows per user):

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
@@ -32,7 +32,8 @@ EXPORTS = ("nais_abi_version", "nais_last_error", "nais_forward", "nais_score_to
            "nais_train_backward_ex", "nais_pair_gather_topk", "nais_topk_keys_finish",
            "nais_pair_prior_table",
            "nais_pair_prior_gather", "nais_topk_blend_rows", "nais_topk_blend_rows_f64",
-           "nais_topk_merge_f64", "nais_train_ucache_size")
+           "nais_topk_merge_f64", "nais_train_ucache_size", "nais_pair_table_split",
+           "nais_pair_bound_topk", "nais_pair_refine_topk")
 
 
 class NaisDotTables(ctypes.Structure):
@@ -223,6 +224,15 @@ def load(path: str | None = None):
     lib.nais_topk_merge_f64.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp]
     lib.nais_topk_keys_finish.restype = i32
     lib.nais_topk_keys_finish.argtypes = [vp, vp, i32, i32, vp, vp, vp, vp]
+    lib.nais_pair_table_split.restype = i32
+    lib.nais_pair_table_split.argtypes = [ctypes.POINTER(NaisParams), vp, i64, i64, i64, vp, vp, vp, vp,
+                                          vp, i64, vp, vp]
+    lib.nais_pair_bound_topk.restype = i32
+    lib.nais_pair_bound_topk.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp, vp,
+                                         i32, vp, vp]
+    lib.nais_pair_refine_topk.restype = i32
+    lib.nais_pair_refine_topk.argtypes = [vp, i64, i64, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32,
+                                          vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32
     lib.nais_stream_create_cu_mask.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
     lib.nais_stream_destroy.restype = i32

@@ -265,10 +265,22 @@ PAIR_TABLE_STREAMS = int(os.environ.get("NAIS_PAIR_TABLE_STREAMS", "2"))
 # the 32 shader engines (auto_table_cus then steps in PAIR_SPLIT_STEP CUs).
 PAIR_WORK_QUEUE = os.environ.get("NAIS_PAIR_WORK_QUEUE", "1") != "0"
 PAIR_SPLIT_STEP = 8
+# Bounded gather + exact refine (round 6; include/nais.h nais_pair_bound_topk): the fused top-k
+# from split16 tables -- the gather streams only their hi halves (4 bytes per history entry and
+# candidate instead of 8), keeps per user the k best LOWER bounds of the exact scores and the
+# candidates whose UPPER bound reaches the k-th of them, and a refine pass recomputes those
+# candidates' exact sums from hi + lo in CSR order: the same lists, ids and score bits as the exact
+# fused gather (tests/test_gpu_bounded.py compares every user). Every block's tables stay resident
+# until the refine (J x P x 8 bytes: 80 GB at config 4), so the route is taken only when they fit
+# the memory budget; otherwise the exact fused gather runs on double-buffered tables.
+PAIR_BOUNDED = True
+PAIR_SURV_CAP = 1024            # survivor keys per user (compacted by the current bound when full)
+PAIR_BOUNDED_STRIPE = 512       # columns per bounded-gather wave (nais_pairs.hip BSTRIPE)
 _masked: dict = {}
 
 
-def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, work_queues=True):
+def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, work_queues=True,
+                   gather_bytes=8):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/, re-fitted in round 3 on the fp16x6 tables:
@@ -290,7 +302,7 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     dist = getattr(model, "VARIANT", 0) in (_capi.VARIANT_REGION_DISTANCE, _capi.VARIANT_DISTANCE)
     D = din - 2 if dist else din
     D = next((w for w in (8, 16, 32, 64, 128) if w >= D), D)   # the padded width the kernels run
-    gbytes = entries * NC * 8.0
+    gbytes = entries * NC * float(gather_bytes)   # 4 on the bounded route (hi words only)
     if prior:
         gbytes *= 2
     xcd = max(1, ncu // 8)
@@ -312,6 +324,10 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     # 256 MB Infinity Cache (config 4: 410 MB), ~51 GB/s from HBM (config-5 shard: 4.1 GB; round 4,
     # 1.64 TB/s on 32 CUs)
     per_cu = 72e9 if block_bytes is None or block_bytes <= 512e6 else 51e9
+    if gather_bytes == 4:
+        # the bounded gather (hi words, 4 B per entry and column): 65 GB/s per CU measured at 64 and
+        # 80 gather CUs (config 4, round 6: 485.8 / 389.3 ms for 2.02 TB; profiles/r6/bounded)
+        per_cu = 65e9
     cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
@@ -444,6 +460,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                          "(the normaliser max G runs over the whole catalog)")
     fused = (PAIR_FUSED_TOPK and not rows_only and J > 0 and k <= 256 and prior is None
              and type(model)._pair_fixup is _NAISDevice._pair_fixup)
+    # the bounded route needs the split16 tables of the NAIS modules' own table kernels
+    bounded_ok = fused and PAIR_BOUNDED and type(model)._pair_table is _NAISDevice._pair_table
     if prior is not None:
         pa, pb, alpha, pc = prior
         pri_coords = torch.as_tensor(np.ascontiguousarray(pc, dtype=np.float64)).to(dev)
@@ -468,6 +486,12 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         return wq_of[h]
 
     def table(tab, c0, w, stream_):
+        if tab.dtype == torch.int32:   # the bounded route's split16 tables
+            _capi.check(lib.nais_pair_table_split(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg),
+                                                  _capi.ptr(cor), _capi.ptr(llm), tab[0].data_ptr(),
+                                                  tab[1].data_ptr(), ld, wq(stream_), stream_),
+                        "nais_pair_table_split")
+            return
         model._pair_table(lib, prm, items, J, c0, w, reg, cor, llm, tab[0].data_ptr(),
                           tab[1].data_ptr(), ld, stream_, work=wq(stream_))
         if prior is not None:
@@ -495,8 +519,11 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         u_dev = u_all[b0:b0 + m]
         if b0 > 0 or m < n:
             J = rows(u_dev, m)
-        def gather_launches(w):   # one fused-gather kernel per 256-column stripe
-            return (w + PAIR_STRIPE - 1) // PAIR_STRIPE if fused else 1
+        bnd = [False]   # this pass takes the bounded route (decided once the tables are sized)
+
+        def gather_launches(w):   # one fused-gather kernel per 256-column (bounded: 512) stripe
+            stripe = PAIR_BOUNDED_STRIPE if bnd[0] else PAIR_STRIPE
+            return (w + stripe - 1) // stripe if fused else 1
         if fused:
             keys = torch.empty(m, k, dtype=torch.int64, device=dev)
             kcount = torch.zeros(m, dtype=torch.int32, device=dev)
@@ -504,6 +531,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             def gather(tab, c0, w, stream_, a=0, b=None):   # launch slots [a, b) of u_dev
                 b = m if b is None else b
                 if b <= a:
+                    return
+                if bnd[0]:
+                    _capi.check(lib.nais_pair_bound_topk(
+                        tab[0].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(), csr.indices.data_ptr(),
+                        u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta), k,
+                        lokeys.data_ptr() + 8 * k * a, locount.data_ptr() + 4 * a,
+                        surv.data_ptr() + 8 * PAIR_SURV_CAP * a, scount.data_ptr() + 4 * a, PAIR_SURV_CAP,
+                        wq(stream_), stream_), "nais_pair_bound_topk")
                     return
                 _capi.check(lib.nais_pair_gather_topk(
                     tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
@@ -534,12 +569,24 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             # when a narrow column shard makes the block width odd
             ld = (W + 3) // 4 * 4
             blocks = list(range(c0_all, c1_all, W))
+            # bounded route: every block's split16 tables (2 x J x ld words each) resident, plus
+            # the per-user lower-bound lists and survivor keys
+            bnd[0] = bounded_ok and (len(blocks) * 2 * J * ld * 4 + m * (PAIR_SURV_CAP + k) * 8
+                                     <= budget)
+            if bnd[0]:
+                arena = torch.empty(len(blocks), 2, J, ld, dtype=torch.int32, device=dev)
+                lokeys = torch.empty(m, k, dtype=torch.int64, device=dev)
+                locount = torch.zeros(m, dtype=torch.int32, device=dev)
+                surv = torch.empty(m, PAIR_SURV_CAP, dtype=torch.int64, device=dev)
+                scount = torch.zeros(m, dtype=torch.int32, device=dev)
+                if events is not None:
+                    events.append(("bounded", None, None, 1))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
             # both streams run as work queues only with the NAIS modules' own table kernel and
             # the fused gather (the score-row gather and nais_dot_pair_table keep fixed grids)
             wq_both = fused and type(model)._pair_table is _NAISDevice._pair_table
             table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None, J * ld * 8,
-                                        work_queues=wq_both)
+                                        work_queues=wq_both, gather_bytes=4 if bnd[0] else 8)
                          if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS)
             wq_on[0] = table_cus % max(1, ncu // 8) != 0
             if events is not None:
@@ -547,8 +594,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 events.append(("block_cols", None, None, W))
             overlap = (0 < table_cus < ncu and len(blocks) > 1 and stream is None
                        and not no_side_streams)
-            tabs = [torch.empty(2, J, ld, dtype=torch.float32, device=dev)
-                    for _ in range(2 if overlap else 1)]
+            tabs = ([] if bnd[0] else [torch.empty(2, J, ld, dtype=torch.float32, device=dev)
+                                       for _ in range(2 if overlap else 1)])
             if prior is not None:
                 pr_of.update({id(t): torch.empty(J, ld, dtype=torch.float64, device=dev) for t in tabs})
             if overlap:
@@ -557,7 +604,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 first_all = PAIR_FIRST_TABLE_ALL_CUS
                 if first_all:      # block 0's table alone, on the caller's stream (all CUs)
                     w0 = min(W, c1_all - blocks[0])
-                    timed("table", lambda: table(tabs[0], blocks[0], w0, st))
+                    tab0 = arena[0] if bnd[0] else tabs[0]
+                    timed("table", lambda: table(tab0, blocks[0], w0, st))
                 for t_ in tss:
                     t_.wait_stream(torch_stream)
                 gs.wait_stream(torch_stream)
@@ -575,10 +623,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     events.append(("gather_share", None, None, share))
             for b, c0 in enumerate(blocks):
                 w = min(W, c1_all - c0)
-                tab = tabs[b % len(tabs)]
+                tab = arena[b] if bnd[0] else tabs[b % len(tabs)]
                 if overlap:
                     tsb = tss[b % len(tss)]
-                    if done_g[b % 2] is not None:
+                    if done_g[b % 2] is not None and not bnd[0]:
                         tsb.wait_event(done_g[b % 2])    # buffer free: its gather finished
                     if not (b == 0 and first_all):
                         e_t0, e_t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -610,9 +658,20 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 torch_stream.wait_stream(gs)
                 for t_ in tss:
                     torch_stream.wait_stream(t_)
-                for t in [*tabs, *pr_of.values(), *([wq_slots] if wq_slots is not None else [])]:
+                for t in [*tabs, *pr_of.values(), *([wq_slots] if wq_slots is not None else []),
+                          *((arena, lokeys, locount, surv, scount) if bnd[0] else ())]:
                     for t_ in (*tss, gs):   # not handed to the main stream early
                         t.record_stream(t_)
+            if bnd[0]:   # the exact refine of every user's surviving candidates (all CUs)
+                stats = torch.zeros(2, dtype=torch.int32, device=dev)
+                timed("refine", lambda: _capi.check(lib.nais_pair_refine_topk(
+                    arena.data_ptr(), 2 * J * ld, J * ld, ld, W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    csr.indices.data_ptr(), u_dev.data_ptr(), m, c0_all, NC, float(model.beta), k,
+                    lokeys.data_ptr(), locount.data_ptr(), surv.data_ptr(), scount.data_ptr(),
+                    PAIR_SURV_CAP, keys.data_ptr(), kcount.data_ptr(), counters[0:1].data_ptr(),
+                    stats.data_ptr(), st), "nais_pair_refine_topk"))
+                model._last_bound_stats = stats
+                del arena, lokeys, locount, surv, scount
             del tabs
             pr_of.clear()
             if not fused:

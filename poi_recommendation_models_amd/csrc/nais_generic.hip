@@ -91,6 +91,7 @@ struct CatArgs {
   float* e;                 // table: e / es [row][ld] (e != nullptr selects the table mode)
   float* es;
   int64_t ld, col0, cols, nitems;
+  uint32_t sel_e, sel_es;   // the table words (float or split16, nais_internal.h)
 };
 
 struct CatLds {
@@ -214,8 +215,9 @@ __global__ void __launch_bounds__(GX_NT, 1) gx_catalog_kernel(GxP p, CatArgs a) 
       if (tab) {
         if (valid && hh == 0 && c < cend) {
           const int64_t o2 = (hbeg + n) * a.ld + (c - a.col0);
-          a.e[o2] = e;
-          a.es[o2] = e * st;
+          const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(e * st);
+          a.e[o2] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, a.sel_e));
+          a.es[o2] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, a.sel_es));
         }
       } else {
         S[t] += gx::half_sum32(e);
@@ -398,7 +400,7 @@ int nais_gx_catalog(const nais_params_t* params, const int64_t* indptr, const in
                     const int32_t* users, int nb, const int64_t* items, int64_t nitems, int64_t col0,
                     int64_t cols, const int64_t* region_of, const double* coords,
                     const double* latlon_mat, float* scores, int64_t score_ld, int32_t* nan_count,
-                    float* e, float* es, int64_t ld, hipStream_t st) {
+                    float* e, float* es, int64_t ld, hipStream_t st, int split) {
   int rc = gx_check(params);
   if (rc) return rc;
   const GxP p = gx_params(params);
@@ -418,6 +420,8 @@ int nais_gx_catalog(const nais_params_t* params, const int64_t* indptr, const in
   a.scores = scores;
   a.score_ld = score_ld;
   a.nan_count = nan_count;
+  a.sel_e = split ? NAIS_SEL_HI : NAIS_SEL_E;
+  a.sel_es = split ? NAIS_SEL_LO : NAIS_SEL_ES;
   auto kern = dist ? gx_catalog_kernel<true> : gx_catalog_kernel<false>;
   if (!e) {   // catalog rows: grid (candidate tiles, users)
     a.indices = indices;

@@ -23,11 +23,19 @@ __attribute__((visibility("hidden"))) int nais_gx_catalog(
     const nais_params_t* params, const int64_t* indptr, const int64_t* indices, const int32_t* users,
     int nb, const int64_t* items, int64_t nitems, int64_t col0, int64_t cols, const int64_t* region_of,
     const double* coords, const double* latlon_mat, float* scores, int64_t score_ld,
-    int32_t* nan_count, float* e, float* es, int64_t ld, hipStream_t st);
+    int32_t* nan_count, float* e, float* es, int64_t ld, hipStream_t st, int split = 0);
 __attribute__((visibility("hidden"))) int nais_gx_forward(
     const nais_params_t* params, const int64_t* hist, int64_t b, int64_t n, int64_t hist_ld,
     const int64_t* target, const int64_t* hreg, int64_t hreg_ld, const int64_t* treg,
     const float* latlon, int64_t ll_ld, float* out, int32_t* nan_count, int32_t flags, hipStream_t st);
+
+// Table words (v_perm_b32 selectors over {S0 = bits of e*s, S1 = bits of e}). The float tables
+// store e and e*s as they are; the split16 tables (nais_pair_table_split) store
+//   hi = [top 16 bits of e*s | top 16 bits of e]   lo = [low 16 bits of e*s | low 16 bits of e]
+// so hi alone gives both values truncated to 8 significant bits (relative error < 2^-7, toward
+// zero; the bounded gather's phase 1) and hi + lo the exact fp32 bits (its refine).
+constexpr uint32_t NAIS_SEL_E = 0x03020100u, NAIS_SEL_ES = 0x07060504u;
+constexpr uint32_t NAIS_SEL_HI = 0x07060302u, NAIS_SEL_LO = 0x05040100u;
 
 // ReLU that keeps NaN, as torch.relu (model.py:71): fmaxf / v_max_f32 would return 0 for a NaN.
 __device__ __forceinline__ float nais_relu(float v) { return (v < 0.f) ? 0.f : v; }

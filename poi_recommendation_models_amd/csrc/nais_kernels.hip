@@ -74,12 +74,16 @@ struct TableOut {
   // work queue (x6n only): the launch's item counter, zeroed before it, and the item grid it covers
   int32_t* work = nullptr;
   int32_t ngroups = 0, ntiles = 0;
+  // the words written to e / es (nais_internal.h): the float tables (e, e*s) or the split16
+  // tables (hi, lo) -- one v_perm_b32 per word, no branch
+  uint32_t sel_e = NAIS_SEL_E, sel_es = NAIS_SEL_ES;
 };
 // the pair's two terms for item row `row` (relative to the launch's base) and column offset x
 __device__ __forceinline__ void tab_put(const TableOut& t, int64_t row, int64_t x, float e, float es) {
   const int64_t o = row * t.ld + x;
-  t.e[o] = e;
-  t.es[o] = es;
+  const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(es);
+  t.e[o] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, t.sel_e));
+  t.es[o] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, t.sel_es));
 }
 
 // Catalog grid: one workgroup per (user slot, 256-POI tile), user-major dispatch order
@@ -1777,8 +1781,10 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     // (the stores as non-temporal or sc1 instead of the default policy, so that the table block
     // being written would not evict the stripe the gather reads from the Infinity Cache: config-4
     // job 0.5968 / 0.5967 / 0.5966 s, base / nt / sc1 means of three interleaved runs, profiles/r5/nt)
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e), re, odd ? (int)0x80000000 : off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(e * sv), rs, odd ? off : (int)0x80000000, 0, 0);
+    // (split16 tables: the hi / lo words of the pair, nais_internal.h; one v_perm_b32 each)
+    const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(e * sv);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(sb, eb, tab.sel_e), re, odd ? (int)0x80000000 : off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(sb, eb, tab.sel_es), rs, odd ? off : (int)0x80000000, 0, 0);
   };
 
   // One unit per step, in block-major order: block m (16 hidden units) takes its KS groups of 12
@@ -3085,7 +3091,7 @@ namespace {
 int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64_t num_items,
                         int64_t col0, int64_t cols, const int64_t* region_of, const double* coords,
                         const double* latlon_mat, float* e, float* es, int64_t ld, int32_t* work,
-                        void* stream) {
+                        void* stream, bool split = false) {
   Shape sh;
   int rc = validate(params, &sh);
   if (rc) return rc;
@@ -3106,8 +3112,12 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
   if (rc) return rc;
   if (sh.gen_tab)
     return nais_gx_catalog(params, nullptr, nullptr, nullptr, 0, items, num_items, col0, cols,
-                           region_of, coords, latlon_mat, nullptr, 0, nullptr, e, es, ld, st);
+                           region_of, coords, latlon_mat, nullptr, 0, nullptr, e, es, ld, st, split);
   TableOut tab;
+  if (split) {
+    tab.sel_e = NAIS_SEL_HI;
+    tab.sel_es = NAIS_SEL_LO;
+  }
   tab.ld = ld;
   tab.cols = cols;
   tab.gi = PAIR_GROUP_ITEMS;
@@ -3142,6 +3152,15 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
                         int64_t ld, int32_t* work, void* stream) {
   return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat, e, es,
                          ld, work, stream);
+}
+
+int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
+                              int64_t col0, int64_t cols, const int64_t* region_of,
+                              const double* coords, const double* latlon_mat, uint32_t* hi,
+                              uint32_t* lo, int64_t ld, int32_t* work, void* stream) {
+  return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat,
+                         reinterpret_cast<float*>(hi), reinterpret_cast<float*>(lo), ld, work, stream,
+                         true);
 }
 
 int32_t nais_score_catalog(const nais_params_t* params, const int64_t* indptr,

@@ -515,6 +515,477 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
   if (lane == 0 && m >= 0.0) atomicMax(gmax + slot, (unsigned long long)__double_as_longlong(m));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Bounded gather + exact refine: the fused top-k of pair_gather_topk_kernel from half its bytes.
+// The tables are split16 (nais_pair_table_split, nais_internal.h): hi[r, c] = the top 16 bits of
+// e and of e*s, lo[r, c] = their low 16 bits. Phase 1 (pair_bound_topk_kernel, one launch per
+// column block) streams only the hi rows -- 4 bytes per (user, history item, candidate) instead
+// of 8 -- and sums, per candidate, S^ = sum e^, N^ = sum es~ and A^ = sum |es~| of the truncated
+// values (e^ <= e < e^ (1 + 2^-7); |e*s - es~| < 2^-7 |es~|, see bound_rows), which bound the
+// exact fp32 sums the exact gather forms:
+//   Sa in [S^ (1 - 3g), S^ (1 + 2^-7)(1 + 3g)],  |Na - N^| <= (2^-7 + 4g) A^,
+// g = h 2^-23 + 2^-20 (the fp32 rounding of either h-term sequential sum, twice over), hence an
+// interval [lo, hi] around the exact score sigmoid(Na / Sa^beta) (widened by 2^-19 in the logit
+// and 2^-20 in the score for the fp32 evaluation of both; a lower logit bound >= 17 means the
+// exact score is 1.0f). Each user keeps the top k LOWER bounds so far (lo_keys: its k-th is a
+// threshold tau that only grows) and appends every candidate whose UPPER bound reaches tau to a
+// survivor list (compacted by the current tau when full; a user whose list overflows is marked
+// -1 and refined over the whole column range). A candidate of the exact top k has exact key >=
+// the k-th exact key >= the final tau (k candidates have exact key >= their lower bound >= tau),
+// so its upper bound reaches every tau on the way: it is a survivor. Phase 2
+// (pair_refine_topk_kernel) recomputes, for each survivor with upper key >= the final tau, the
+// exact Na and Sa from hi + lo in history (CSR) order -- the exact gather's operations on the
+// same fp32 bits -- and ranks them: the same top-k lists, ids and score bits, as the exact gather.
+// Keys as pair_gather_topk_kernel: ordered(score) << 32 | (0xFFFFFFFF - poi).
+constexpr int BCPL = 8;                       // columns per lane: 32-byte hi rows per lane
+constexpr int BSTRIPE = 64 * BCPL;            // 512 columns per wave (one launch per block)
+constexpr int BK_LDS = 512;                   // keys per wave in LDS: k + 256 offered (k <= 256)
+constexpr uint32_t SEL_REC_E = 0x05040100u;   // perm(hi, lo): [hi.lo16 | lo.lo16] = bits of e
+constexpr uint32_t SEL_REC_ES = 0x07060302u;  // perm(hi, lo): [hi.hi16 | lo.hi16] = bits of e*s
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// S^ += e^, N^ += es~, A^ += |es~| over the jn rows whose item rows lanes 0..jn-1 hold (CSR order).
+// e^ = hi << 16 is e truncated to its top 16 bits; es~ is the hi word itself read as a float: the
+// top 16 bits of e*s followed by those of e, so |es~| and |e*s| both lie in [|es^|, |es^| + ulp16)
+// with the sign of e*s -- |e*s - es~| < 2^-7 |es~|, the bound the refine threshold assumes. Rows
+// are read through a buffer resource on the row's base (scalar: readlane of the row, s_mul) with
+// the lane's constant column offset, so a row costs no VALU for its address, and the bytes past
+// the launch's columns read as 0 (num_records), which adds nothing. S and N take v_pk_add_f32.
+__device__ __forceinline__ void bound_rows(const uint32_t* __restrict__ HI, int64_t ld, int32_t mrow,
+                                           int jn, uint32_t colbytes, uint32_t voff, f2v (&S)[BCPL / 2],
+                                           f2v (&N)[BCPL / 2], float (&A)[BCPL]) {
+  auto row = [&](int jj) __attribute__((always_inline)) {
+    const int64_t r = __builtin_amdgcn_readlane(mrow, jj);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(HI) + r * ld, (short)0, (int)colbytes,
+                                             0x00020000);
+  };
+  auto acc = [&](const uint4 (&v)[2]) __attribute__((always_inline)) {
+    const uint32_t w[BCPL] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+    for (int q = 0; q < BCPL; q += 2) {
+      S[q / 2] += f2v{__uint_as_float(w[q] << 16), __uint_as_float(w[q + 1] << 16)};
+      N[q / 2] += f2v{__uint_as_float(w[q]), __uint_as_float(w[q + 1])};
+      A[q] += fabsf(__uint_as_float(w[q]));
+      A[q + 1] += fabsf(__uint_as_float(w[q + 1]));
+    }
+  };
+  auto ld2 = [&](__amdgpu_buffer_rsrc_t rs, uint4 (&v)[2]) __attribute__((always_inline)) {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, 0, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff + 16, 0, 0);
+    v[0] = uint4{a[0], a[1], a[2], a[3]};
+    v[1] = uint4{b[0], b[1], b[2], b[3]};
+  };
+  int jj = 0;
+  for (; jj + GU <= jn; jj += GU) {
+    uint4 v[GU][2];
+#pragma unroll
+    for (int g = 0; g < GU; ++g) ld2(row(jj + g), v[g]);
+#pragma unroll
+    for (int g = 0; g < GU; ++g) acc(v[g]);
+  }
+  for (; jj < jn; ++jj) {
+    uint4 v[2];
+    ld2(row(jj), v);
+    acc(v);
+  }
+}
+
+__device__ __forceinline__ float sigmoid_ref(float l) { return 1.0f / (1.0f + expf(-l)); }
+__device__ __forceinline__ unsigned long long score_key(float sc, int64_t c) {
+  return ((unsigned long long)ord_f32_p(sc) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)c);
+}
+constexpr unsigned long long KEY_SCORE_MAX = 0xFFFFFFFF00000000ull;   // above every score's key
+
+// The interval of one candidate's exact score from its truncated sums (see above). hl == 0: the
+// exact score 0.5 (logit 0). Returns false when the sums do not bound it (a zero or overflowing
+// S^, non-finite sums): the candidate is then refined whatever tau is.
+struct Bounds {
+  float slo, shi, nlo, nhi, dlo, dhi;
+  bool ok;
+};
+__device__ __forceinline__ Bounds make_bounds(float S, float N, float A, int64_t hl, float beta) {
+  Bounds b;
+  const float g = (float)hl * 0x1p-23f + 0x1p-20f;
+  const float tiny = (float)hl * 0x1p-126f;   // truncation below the normal range (absolute)
+  b.slo = S * (1.f - 3.f * g);
+  b.shi = S * (1.f + 0x1p-7f) * (1.f + 3.f * g) + tiny;
+  const float rn = (0x1p-7f + 4.f * g) * A + tiny;
+  b.nlo = N - rn;
+  b.nhi = N + rn;
+  if (beta == 0.5f) {
+    b.dlo = sqrtf(b.slo);
+    b.dhi = sqrtf(b.shi);
+  } else {
+    const float p0 = powf(b.slo, beta), p1 = powf(b.shi, beta);
+    b.dlo = fminf(p0, p1);
+    b.dhi = fmaxf(p0, p1);
+  }
+  b.ok = b.slo > 0.f && b.dlo > 0.f && __builtin_isfinite(b.dhi) && __builtin_isfinite(b.nlo) &&
+         __builtin_isfinite(b.nhi);
+  return b;
+}
+__device__ __forceinline__ float upper_score(const Bounds& b) {
+  float l = b.nhi >= 0.f ? b.nhi / b.dlo : b.nhi / b.dhi;
+  l += fabsf(l) * 0x1p-19f;
+  return fminf(sigmoid_ref(l) * (1.f + 0x1p-20f), 1.0f);
+}
+__device__ __forceinline__ float lower_score(const Bounds& b) {
+  float l = b.nlo >= 0.f ? b.nlo / b.dhi : b.nlo / b.dlo;
+  l -= fabsf(l) * 0x1p-19f;
+  return l >= 17.f ? 1.0f : sigmoid_ref(l) * (1.f - 0x1p-20f);
+}
+
+// A cheap test that a candidate cannot reach the list's k-th key: its upper logit (v_rcp / v_sqrt,
+// widened by 2^-17 to cover them and the accurate path's own rounding) is below L, the logit under
+// which the accurate upper score stays below the k-th key's score (lthr_of). beta == 0.5 only
+// (else L = -inf: no pruning); NaN anywhere keeps the candidate.
+__device__ __forceinline__ bool may_reach(float S, float N, float A, int64_t hl, float L) {
+  const float g = (float)hl * 0x1p-23f + 0x1p-20f;
+  const float tiny = (float)hl * 0x1p-126f;
+  const float nhi = N + ((0x1p-7f + 4.f * g) * A + tiny);
+  const float sd = nhi >= 0.f ? S * (1.f - 3.f * g) : S * (1.f + 0x1p-7f) * (1.f + 3.f * g) + tiny;
+  float l = nhi * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(sd));
+  l += fabsf(l) * 0x1p-17f;
+  return !(l < L);
+}
+// L for may_reach from the k-th key's score ts: upper_score(l) <= sigmoid_fp32(l) (1 + 2^-20) <
+// ts for every l < L = logit(ts (1 - 2^-18)) less a margin (ts = 1.0f: L ~ 12.5, below which the
+// upper score is < 1.0f). -inf when there is no such bound (list not full, ts <= 0, NaN, beta).
+__device__ __forceinline__ float lthr_of(unsigned long long thr, float beta) {
+  if (thr == 0ull || beta != 0.5f) return -__builtin_inff();
+  const float ts = unord_f32_p((uint32_t)(thr >> 32));
+  if (!(ts > 0.f && ts <= 1.f)) return -__builtin_inff();
+  const double p = (double)ts * (1.0 - 0x1p-18);
+  double L = log(p / (1.0 - p));
+  L -= 1e-6 * (1.0 + fabs(L));
+  return (float)L;
+}
+
+// Merges the keys kq[q] with bit q of `offer` set (this lane's) into the wave's descending list
+// L[0 .. cnt) in LDS; L has room for the padded power of two of cnt + offered. Returns the new
+// count min(cnt + offered, k); L[0 .. that) is the new list.
+template <int NQ>
+__device__ int wave_merge_keys(unsigned long long* L, int cnt, const unsigned long long (&kq)[NQ],
+                               uint32_t offer, int k) {
+  const int lane = threadIdx.x & 63;
+  const int mine_n = __popc(offer);
+  int excl = mine_n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(excl, o);
+    if (lane >= o) excl += y;
+  }
+  const int m = __shfl(excl, 63);
+  excl -= mine_n;
+  if (m == 0) return cnt;
+  int pos = cnt + excl;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+    if ((offer >> q) & 1u) L[pos++] = kq[q];
+  const int n = cnt + m;
+  int n2 = 64;
+  while (n2 < n) n2 <<= 1;
+  for (int i = n + lane; i < n2; i += 64) L[i] = 0ull;
+  wave_lds_sync();
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < n2; i += 64) {
+        const int partner = i ^ stride;
+        if (partner > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long a = L[i], b = L[partner];
+          if (desc ? (a < b) : (a > b)) {
+            L[i] = b;
+            L[partner] = a;
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  return n < k ? n : k;
+}
+
+__global__ void __launch_bounds__(GW * 64)
+pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_t* __restrict__ rowmap,
+                       const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
+                       const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
+                       float beta, int k, unsigned long long* __restrict__ lokeys,
+                       int32_t* __restrict__ locount, unsigned long long* __restrict__ surv,
+                       int32_t* __restrict__ scount, int cap, int32_t* __restrict__ work) {
+  __shared__ unsigned long long lk[GW][BK_LDS];
+  __shared__ uint32_t hm[GW][BSTRIPE / 32];   // history POIs of this block, one bit per column
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int GQ = 4;
+  int64_t qnext = 0, qend = 0;
+  for (int64_t it = 0;; ++it) {
+  int64_t slot;
+  if (work) {
+    if (qnext == qend) {
+      int got = 0;
+      if (lane == 0) got = atomicAdd(work, GQ);
+      qnext = __builtin_amdgcn_readfirstlane(got);
+      qend = qnext + GQ;
+    }
+    slot = qnext++;
+  } else {
+    if (it > 0) break;
+    slot = int64_t(blockIdx.x) * GW + w;
+  }
+  if (slot >= nusers) break;                 // wave-uniform; no workgroup barriers below
+  const int64_t u = users[slot];
+  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  const int64_t x = int64_t(lane) * BCPL;    // column within the block [col0, col0 + cols)
+  if (lane < BSTRIPE / 32) hm[w][lane] = 0u;
+  wave_lds_sync();
+  f2v S2[BCPL / 2], N2[BCPL / 2];
+  float A[BCPL];
+#pragma unroll
+  for (int q = 0; q < BCPL / 2; ++q) S2[q] = N2[q] = f2v{0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < BCPL; ++q) A[q] = 0.f;
+  for (int64_t j0 = 0; j0 < hl; j0 += 64) {
+    const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
+    int32_t mrow = 0;
+    if (lane < jn) {
+      const int64_t c = indices[hb + j0 + lane];
+      mrow = rowmap[c];
+      const int64_t r = c - col0;
+      if (r >= 0 && r < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
+    }
+    bound_rows(HI, ld, mrow, jn, (uint32_t)(cols * 4), (uint32_t)(x * 4), S2, N2, A);
+  }
+  wave_lds_sync();
+  float S[BCPL], N[BCPL];
+#pragma unroll
+  for (int q = 0; q < BCPL; ++q) {
+    S[q] = S2[q / 2][q & 1];
+    N[q] = N2[q / 2][q & 1];
+  }
+  const int cnt = locount[slot];
+  const unsigned long long thr = cnt == k ? lokeys[slot * k + k - 1] : 0ull;   // valid keys are > 0
+  // upper keys of every candidate; lower keys only where the upper one reaches thr (else neither
+  // can enter the list nor survive). Held as their score halves (the id half is the column's), so
+  // the epilogue does not outgrow the gather loop's registers.
+  uint32_t ho[BCPL], lo_[BCPL];
+  uint32_t live = 0, offer = 0;
+  const uint32_t idb0 = 0xFFFFFFFFu - (uint32_t)(col0 + x);   // id half of column x; x + q: - q
+  auto key_of = [&](uint32_t ord, int q) __attribute__((always_inline)) {
+    return ((unsigned long long)ord << 32) | (unsigned long long)(idb0 - (uint32_t)q);
+  };
+  const float Lthr = lthr_of(thr, beta);   // wave-uniform
+#pragma unroll
+  for (int q = 0; q < BCPL; ++q) {
+    ho[q] = 0u;
+    lo_[q] = 0u;
+    const int64_t r = x + q;
+    if (r < cols && !((hm[w][r >> 5] >> (r & 31)) & 1u)) {
+      if (hl == 0) {   // exact: logit 0 -> 0.5 for every candidate
+        live |= 1u << q;
+        ho[q] = lo_[q] = ord_f32_p(0.5f);
+      } else if (may_reach(S[q], N[q], A[q], hl, Lthr)) {
+        live |= 1u << q;
+        const Bounds b = make_bounds(S[q], N[q], A[q], hl, beta);
+        ho[q] = b.ok ? ord_f32_p(upper_score(b)) : 0xFFFFFFFFu;
+        if (b.ok && key_of(ho[q], q) > thr) lo_[q] = ord_f32_p(lower_score(b));
+      }
+      if (lo_[q] != 0u && key_of(lo_[q], q) > thr) offer |= 1u << q;
+    }
+  }
+  // the list of lower bounds: two merges of <= 256 offered keys (the LDS holds k + 256)
+  unsigned long long* L = lk[w];
+  int nk = cnt;
+  const bool merged = __ballot(offer != 0u) != 0ull;
+  if (merged) {
+    for (int i = lane; i < cnt; i += 64) L[i] = lokeys[slot * k + i];
+    wave_lds_sync();
+    const unsigned long long l0[4] = {key_of(lo_[0], 0), key_of(lo_[1], 1), key_of(lo_[2], 2), key_of(lo_[3], 3)};
+    const unsigned long long l1[4] = {key_of(lo_[4], 4), key_of(lo_[5], 5), key_of(lo_[6], 6), key_of(lo_[7], 7)};
+    nk = wave_merge_keys<4>(L, nk, l0, offer & 0xFu, k);
+    nk = wave_merge_keys<4>(L, nk, l1, offer >> 4, k);
+    for (int i = lane; i < nk; i += 64) lokeys[slot * k + i] = L[i];
+    if (lane == 0) locount[slot] = nk;
+  }
+  const unsigned long long tau = nk == k ? (merged ? L[k - 1] : thr) : 0ull;
+  // survivors: upper key >= tau, appended to the user's list
+  uint32_t sv = 0;
+#pragma unroll
+  for (int q = 0; q < BCPL; ++q)
+    if (((live >> q) & 1u) && key_of(ho[q], q) >= tau) sv |= 1u << q;
+  const int mine_n = __popc(sv);
+  int excl = mine_n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(excl, o);
+    if (lane >= o) excl += y;
+  }
+  const int m = __shfl(excl, 63);
+  excl -= mine_n;
+  int sc = scount[slot];
+  if (m > 0 && sc >= 0) {
+    unsigned long long* list = surv + slot * (int64_t)cap;
+    if (sc + m > cap) {   // compact by the current tau (in place: a write never passes the chunk read)
+      int wpos = 0;
+      for (int i0 = 0; i0 < sc; i0 += 64) {
+        const bool in = i0 + lane < sc;
+        const unsigned long long v = in ? list[i0 + lane] : 0ull;
+        const bool keep = in && v >= tau;
+        const unsigned long long bal = __ballot(keep);
+        const int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (keep) list[wpos + before] = v;
+        wpos += __popcll(bal);
+      }
+      sc = wpos + m > cap ? -1 : wpos;   // -1: overflow, refined over the whole column range
+    }
+    if (sc >= 0) {
+      int pos = sc + excl;
+#pragma unroll
+      for (int q = 0; q < BCPL; ++q)
+        if ((sv >> q) & 1u) list[pos++] = key_of(ho[q], q);
+      sc += m;
+    }
+    if (lane == 0) scount[slot] = sc;
+  }
+  wave_lds_sync();   // the next slot's hm / lk writers after this slot's readers
+  }
+}
+
+// Phase 2: per user, the exact scores of the candidates whose upper key reaches the final tau (all
+// columns of [col0, col0 + cols) for an overflowed user), from hi + lo of the block tables
+//   tables + b * bstride + row * ld + x  (hi),  + lo_off (lo),  column col0 + b * bcols + x,
+// summed in history (CSR) order as pair_gather_topk_kernel sums them, 64 candidates (one per lane)
+// at a time; a running top-k in LDS. stats[0] += candidates refined, stats[1] += overflowed users.
+constexpr int RF_LDS = 512;   // running list (k <= 256) + 64 offered, padded to a power of two
+
+__global__ void __launch_bounds__(GW * 64)
+pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t lo_off, int64_t ld,
+                        int64_t bcols, const int32_t* __restrict__ rowmap,
+                        const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
+                        const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
+                        float beta, int k, const unsigned long long* __restrict__ lokeys,
+                        const int32_t* __restrict__ locount, const unsigned long long* __restrict__ surv,
+                        const int32_t* __restrict__ scount, int cap, unsigned long long* __restrict__ keys,
+                        int32_t* __restrict__ kcount, int32_t* __restrict__ nan_count,
+                        int32_t* __restrict__ stats) {
+  __shared__ unsigned long long lk[GW][RF_LDS];
+  __shared__ uint32_t cb[GW][128];   // pending candidate columns (relative to col0)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t slot = int64_t(blockIdx.x) * GW + w;
+  if (slot >= nusers) return;                // wave-uniform; no workgroup barriers below
+  const int64_t u = users[slot];
+  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  const int cnt = locount[slot];
+  const unsigned long long tau = cnt == k ? lokeys[slot * k + k - 1] : 0ull;
+  const int sc = scount[slot];
+  unsigned long long* L = lk[w];
+  int nk = 0;             // the running exact list L[0 .. nk)
+  int nan = 0, refined = 0;
+  // exact keys of the columns r (valid lanes) -> merged into L
+  auto batch = [&](int64_t r, bool valid) __attribute__((always_inline)) {
+    const int64_t rr = valid ? r : 0;                   // invalid lanes read a column that exists
+    const int64_t b = rr / bcols;
+    const int64_t xo = b * bstride + (rr - b * bcols);
+    const int64_t c = col0 + rr;
+    float Sa = 0.f, Na = 0.f;
+    bool in_hist = false;
+    for (int64_t j0 = 0; j0 < hl; j0 += 64) {
+      const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
+      int64_t mine = 0, mid = -1;
+      if (lane < jn) {
+        mid = indices[hb + j0 + lane];
+        mine = int64_t(rowmap[mid]) * ld;
+      }
+      const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
+      const uint32_t ilo = uint32_t(mid), ihi = uint32_t(mid >> 32);
+      int jj = 0;
+      for (; jj + GU <= jn; jj += GU) {
+        uint32_t h[GU], l[GU];
+        int64_t id[GU];
+#pragma unroll
+        for (int g = 0; g < GU; ++g) {
+          const int64_t o = bcast64(mlo, mhi, jj + g) + xo;
+          id[g] = bcast64(ilo, ihi, jj + g);
+          h[g] = T[o];
+          l[g] = T[o + lo_off];
+        }
+#pragma unroll
+        for (int g = 0; g < GU; ++g) {
+          Sa += __uint_as_float(__builtin_amdgcn_perm(h[g], l[g], SEL_REC_E));
+          Na += __uint_as_float(__builtin_amdgcn_perm(h[g], l[g], SEL_REC_ES));
+          in_hist |= id[g] == c;
+        }
+      }
+      for (; jj < jn; ++jj) {
+        const int64_t o = bcast64(mlo, mhi, jj) + xo;
+        const uint32_t h = T[o], l = T[o + lo_off];
+        Sa += __uint_as_float(__builtin_amdgcn_perm(h, l, SEL_REC_E));
+        Na += __uint_as_float(__builtin_amdgcn_perm(h, l, SEL_REC_ES));
+        in_hist |= bcast64(ilo, ihi, jj) == c;
+      }
+    }
+    unsigned long long kq[1] = {0ull};
+    uint32_t offer = 0;
+    if (valid && !in_hist) {
+      float logit = 0.f;   // empty history: logit 0
+      if (hl > 0) logit = Na / ((beta == 0.5f) ? sqrtf(Sa) : powf(Sa, beta));
+      float s = 1.0f / (1.0f + expf(-logit));
+      if (logit != logit) {
+        s = __builtin_nanf("");
+        ++nan;
+      }
+      kq[0] = score_key(s, c);
+      ++refined;
+      const unsigned long long lthr = nk == k ? L[k - 1] : 0ull;
+      if (kq[0] > lthr) offer = 1u;
+    }
+    wave_lds_sync();
+    nk = wave_merge_keys<1>(L, nk, kq, offer, k);
+  };
+  if (sc < 0) {   // overflowed: every column of the range
+    for (int64_t r0 = 0; r0 < cols; r0 += 64) batch(r0 + lane, r0 + lane < cols);
+  } else {
+    const unsigned long long* list = surv + slot * (int64_t)cap;
+    int pend = 0;   // cb[w][0 .. pend)
+    for (int i0 = 0; i0 < sc; i0 += 64) {
+      const bool in = i0 + lane < sc;
+      const unsigned long long v = in ? list[i0 + lane] : 0ull;
+      const bool keep = in && v >= tau;
+      const unsigned long long bal = __ballot(keep);
+      if (keep) cb[w][pend + __popcll(bal & ((1ull << lane) - 1ull))] =
+          (uint32_t)((0xFFFFFFFFu - (uint32_t)(v & 0xFFFFFFFFull)) - (uint32_t)col0);
+      pend += __popcll(bal);
+      wave_lds_sync();
+      if (pend >= 64) {
+        const uint32_t r = cb[w][lane];
+        const uint32_t rest = lane < pend - 64 ? cb[w][64 + lane] : 0u;
+        wave_lds_sync();
+        if (lane < pend - 64) cb[w][lane] = rest;
+        pend -= 64;
+        wave_lds_sync();
+        batch((int64_t)r, true);
+      }
+    }
+    if (pend > 0) {
+      const uint32_t r = lane < pend ? cb[w][lane] : 0u;
+      batch((int64_t)r, lane < pend);
+    }
+  }
+  for (int i = lane; i < nk; i += 64) keys[slot * k + i] = L[i];
+  if (lane == 0) kcount[slot] = nk;
+  if (nan_count) {
+    for (int o = 32; o > 0; o >>= 1) nan += __shfl_xor(nan, o);
+    if (lane == 0 && nan) atomicAdd(nan_count, nan);
+  }
+  if (stats) {
+    for (int o = 32; o > 0; o >>= 1) refined += __shfl_xor(refined, o);
+    if (lane == 0) {
+      atomicAdd(stats, refined);
+      if (sc < 0) atomicAdd(stats + 1, 1);
+    }
+  }
+}
+
 // keys -> (ids, scores) of the top-k lists; short lists padded with -1 / NaN and counted
 __global__ void topk_keys_finish_kernel(const unsigned long long* __restrict__ keys,
                                         const int32_t* __restrict__ kcount, int32_t n, int k,
@@ -622,6 +1093,65 @@ int32_t nais_pair_gather_topk(const float* e, const float* es, int64_t ld, const
     if (rc) return rc;
   }
   return NAIS_OK;
+}
+
+int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowmap,
+                             const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                             int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                             uint64_t* lo_keys, int32_t* lo_count, uint64_t* surv, int32_t* surv_count,
+                             int32_t surv_cap, int32_t* work, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || k <= 0 || surv_cap < 64)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (k > BK_LDS - 256) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
+  if (col0 + cols > 0xFFFFFFFFll) return nais_internal_fail(NAIS_E_UNSUPPORTED, "POI ids must fit 32 bits");
+  if (num_users == 0 || cols == 0) return NAIS_OK;
+  if (!hi || !rowmap || !indptr || !indices || !users || !lo_keys || !lo_count || !surv || !surv_count)
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  if (ld % 4 != 0 || (reinterpret_cast<uintptr_t>(hi) & 15) != 0)
+    return nais_internal_fail(NAIS_E_INVALID, "ld must be a multiple of 4 and hi 16-byte aligned");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  unsigned groups = (unsigned)((num_users + GW - 1) / GW);
+  if (work) {   // a work queue: one resident round of workgroups on the stream's CUs (5 per CU)
+    const int ncu = nais_internal_stream_cus(st);
+    if (ncu <= 0) return nais_internal_fail(NAIS_E_HIP, "device attributes");
+    groups = std::min<unsigned>(groups, (unsigned)ncu * 5u);
+  }
+  for (int64_t s0 = 0; s0 < cols; s0 += BSTRIPE) {   // one launch per stripe: one writer per list
+    if (work && hipMemsetAsync(work, 0, sizeof(int32_t), st) != hipSuccess)
+      return nais_internal_fail(NAIS_E_HIP, "hipMemsetAsync(work)");
+    hipLaunchKernelGGL(pair_bound_topk_kernel, dim3(groups), dim3(GW * 64), 0, st, hi + s0, ld, rowmap,
+                       indptr, indices, users, num_users, col0 + s0, std::min<int64_t>(BSTRIPE, cols - s0),
+                       beta, (int)k, reinterpret_cast<unsigned long long*>(lo_keys), lo_count,
+                       reinterpret_cast<unsigned long long*>(surv), surv_count, (int)surv_cap, work);
+    const int32_t rc = nais_internal_check_launch("pair_bound_topk_kernel");
+    if (rc) return rc;
+  }
+  return NAIS_OK;
+}
+
+int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int64_t lo_offset,
+                              int64_t ld, int64_t block_cols, const int32_t* rowmap,
+                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
+                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
+                              const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
+                              const int32_t* surv_count, int32_t surv_cap, uint64_t* keys,
+                              int32_t* kcount, int32_t* nan_count, int32_t* stats, void* stream) {
+  if (num_users < 0 || col0 < 0 || cols < 0 || k <= 0 || surv_cap < 64 || block_cols <= 0 ||
+      ld < std::min<int64_t>(block_cols, cols) || lo_offset < 0 || block_stride < 0)
+    return nais_internal_fail(NAIS_E_INVALID, "bad shape");
+  if (k > RF_LDS - 256) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
+  if (col0 + cols > 0xFFFFFFFFll) return nais_internal_fail(NAIS_E_UNSUPPORTED, "POI ids must fit 32 bits");
+  if (num_users == 0) return NAIS_OK;
+  if (!rowmap || !indptr || !indices || !users || !lo_keys || !lo_count || !surv || !surv_count ||
+      !keys || !kcount || (cols > 0 && !tables))
+    return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
+  hipLaunchKernelGGL(pair_refine_topk_kernel, dim3((unsigned)((num_users + GW - 1) / GW)), dim3(GW * 64), 0,
+                     reinterpret_cast<hipStream_t>(stream), tables, block_stride, lo_offset, ld, block_cols,
+                     rowmap, indptr, indices, users, num_users, col0, cols, beta, (int)k,
+                     reinterpret_cast<const unsigned long long*>(lo_keys), lo_count,
+                     reinterpret_cast<const unsigned long long*>(surv), surv_count, (int)surv_cap,
+                     reinterpret_cast<unsigned long long*>(keys), kcount, nan_count, stats);
+  return nais_internal_check_launch("pair_refine_topk_kernel");
 }
 
 int32_t nais_pair_prior_table(const double* coords, int64_t num_pois, const int64_t* items,

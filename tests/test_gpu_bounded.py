@@ -1,0 +1,171 @@
+"""GPU: the bounded gather + exact refine (catalog.PAIR_BOUNDED; include/nais.h
+nais_pair_table_split / nais_pair_bound_topk / nais_pair_refine_topk) returns the exact fused
+gather's top-k -- the same ids and the same score bits -- for every user.
+
+The split16 tables hold the float tables' bits (hi + lo), checked per table kernel; the bounded
+route is then compared with the exact route (PAIR_BOUNDED off: nais_pair_gather_topk on the float
+tables) on whole jobs, including the shapes that stress the bounds: score clusters (the
+reference's N(0, 0.01) init puts every score near sigmoid(0)), saturated scores (ties at 1.0f broken
+by POI id), beta != 0.5 (powf), empty histories, fewer candidates than k, a column shard, and a
+survivor list too small for its band (the overflow path refines every column)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _model(P, D, H, variant="basic", seed=3, emb_std=0.3, beta=0.5, precision="fp16x6"):
+    from poi_recommendation_models_amd import model as M
+    from poi_recommendation_models_amd.synthetic import init_nais_params
+    if variant == "basic":
+        m = M.NAIS_basic(P, D, H, beta)
+    else:
+        m = M.NAIS_region_distance_Embedding(P, D, H, beta, 64, 1)
+    p = init_nais_params(P, D, H, seed=seed, emb_std=emb_std, bias_std=0.1, variant=variant, num_regions=64)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()}, strict=False)
+    m.precision = precision
+    m.report_nan = False
+    return m.to(DEV).eval()
+
+
+def _run(m, data, k, bounded, users=None, cols=None, side=None):
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, data.num_pois, DEV)
+    users = np.arange(data.num_users) if users is None else users
+    old = catalog.PAIR_BOUNDED
+    catalog.PAIR_BOUNDED = bounded
+    try:
+        side = side or (None, None, None)
+        ev = []
+        ids, sc = _score_topk_pairs(m, csr, users, k, *side, None, force=True, cols=cols, events=ev)
+    finally:
+        catalog.PAIR_BOUNDED = old
+    torch.cuda.synchronize()
+    took = any(kind == "bounded" for kind, *_ in ev)
+    return ids.cpu().numpy(), sc.cpu().numpy(), int(m._last_nan.item()), took
+
+
+def _same(a, b):
+    ia, sa, na, ta = a
+    ib, sb, nb, tb = b
+    assert ta and not tb, "routes: bounded %s, exact %s" % (ta, tb)
+    np.testing.assert_array_equal(ia, ib)
+    np.testing.assert_array_equal(sa.view(np.uint32), sb.view(np.uint32))   # the same bits
+    assert na == nb
+
+
+@pytest.mark.parametrize("variant,precision,D,H", [("basic", "fp16x6", 64, 64), ("basic", "fp32", 32, 32),
+                                                   ("basic", "fp16x3", 64, 64), ("basic", "fp16x6", 100, 40),
+                                                   ("region_distance", "fp16x6", 64, 64)])
+def test_split_tables_hold_the_float_bits(variant, precision, D, H):
+    from poi_recommendation_models_amd import _capi
+    P, J, W = 3000, 300, 512
+    m = _model(P, D, H, variant, precision=precision)
+    lib = _capi.load()
+    prm = m._score_params()
+    items = torch.arange(5, 5 + J, dtype=torch.int64, device=DEV)
+    reg = torch.as_tensor(np.arange(P) % 64, dtype=torch.int64, device=DEV)
+    rng = np.random.default_rng(0)
+    cor = torch.as_tensor(np.stack([35.5 + 0.3 * rng.random(P), 139.4 + 0.4 * rng.random(P)], 1), device=DEV)
+    dist = variant == "region_distance"
+    side = (reg if variant != "basic" else None, cor if dist else None)
+    for c0 in (0, 700, P - 200):
+        w = min(W, P - c0)
+        f = torch.zeros(2, J, W, dtype=torch.float32, device=DEV)
+        t = torch.zeros(2, J, W, dtype=torch.int32, device=DEV)
+        _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, w, _capi.ptr(side[0]), _capi.ptr(side[1]),
+                                        None, f[0].data_ptr(), f[1].data_ptr(), W, None, None), "table")
+        _capi.check(lib.nais_pair_table_split(prm, items.data_ptr(), J, c0, w, _capi.ptr(side[0]),
+                                              _capi.ptr(side[1]), None, t[0].data_ptr(), t[1].data_ptr(), W,
+                                              None, None), "table_split")
+        torch.cuda.synchronize()
+        fb = f.cpu().numpy().view(np.uint32)
+        hi, lo = (x.astype(np.uint32) for x in t.cpu().numpy().view(np.uint32))
+        e = (hi << 16) | (lo & 0xFFFF)
+        es = (hi & 0xFFFF0000) | (lo >> 16)
+        np.testing.assert_array_equal(e[:, :w], fb[0][:, :w])
+        np.testing.assert_array_equal(es[:, :w], fb[1][:, :w])
+
+
+@pytest.mark.parametrize("case", ["bench_like", "reference_init", "beta07", "k1_k256", "region_distance",
+                                  "fp32", "generic_shape"])
+def test_bounded_route_equals_exact_route(case):
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    P, U, hmax, k, D, H = 12000, 1500, 200, 50, 64, 64
+    kw = {}
+    if case == "reference_init":
+        kw = dict(emb_std=0.01)         # model.py:30-35: every score within ~1e-4 of 0.5
+    elif case == "beta07":
+        kw = dict(beta=0.7)
+    elif case == "fp32":
+        kw = dict(precision="fp32")
+        D = H = 32
+    elif case == "generic_shape":
+        D, H = 100, 40
+    variant = "region_distance" if case == "region_distance" else "basic"
+    data = make_checkins(U, P, hmax, seed=11)
+    m = _model(P, D, H, variant, **kw)
+    side = None
+    if variant == "region_distance":
+        side = (np.arange(P) % 64, data.place_coords, None)
+    for kk in ((1, 256) if case == "k1_k256" else (k,)):
+        _same(_run(m, data, kk, True, side=side), _run(m, data, kk, False, side=side))
+    st = m._last_bound_stats.cpu().numpy() if hasattr(m, "_last_bound_stats") else None
+    print(case, "refined per user", None if st is None else st[0] / U, "overflowed", None if st is None else st[1])
+
+
+def test_bounded_route_saturated_scores_ties_by_id():
+    """Trained-like magnitudes: many candidates score exactly 1.0f, ranked by POI id."""
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    data = make_checkins(300, 6000, 60, seed=5)
+    m = _model(6000, 32, 32, emb_std=3.0)
+    b = _run(m, data, 50, True)
+    assert (b[1] == 1.0).mean() > 0.5, "the case must saturate"
+    _same(b, _run(m, data, 50, False))
+
+
+def test_bounded_route_edge_users():
+    """Empty histories (every score 0.5), a user with fewer candidates than k, long histories."""
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    data = make_checkins(400, 3000, 120, seed=9)
+    hist = [data.history(u) for u in range(data.num_users)]
+    hist[3] = np.zeros(0, np.int64)
+    hist[7] = np.zeros(0, np.int64)
+    hist[11] = np.arange(0, 3000 - 30, dtype=np.int64)        # 30 candidates (k = 50 > 30)
+    hist[12] = np.sort(np.random.default_rng(1).choice(3000, 1500, replace=False))
+    data.indptr = np.concatenate([[0], np.cumsum([len(h) for h in hist])]).astype(np.int64)
+    data.indices = np.concatenate(hist).astype(np.int64)
+    m = _model(3000, 32, 32)
+    users = np.array([u for u in range(data.num_users) if u != 11])
+    _same(_run(m, data, 50, True, users=users), _run(m, data, 50, False, users=users))
+    # user 11 alone has fewer candidates than k: column shards allow it (short lists padded)
+    _same(_run(m, data, 50, True, cols=(0, 3000)), _run(m, data, 50, False, cols=(0, 3000)))
+
+
+def test_bounded_route_column_shard():
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    data = make_checkins(800, 9000, 100, seed=13)
+    m = _model(9000, 64, 64)
+    for cols in ((0, 4500), (4500, 9000), (1234, 5001)):
+        _same(_run(m, data, 50, True, cols=cols), _run(m, data, 50, False, cols=cols))
+
+
+def test_bounded_route_overflow_refines_every_column():
+    """A survivor list of 64 keys cannot hold the first block's band at k = 60: the users overflow
+    and the refine takes every column, with the same result."""
+    from poi_recommendation_models_amd import catalog
+    from poi_recommendation_models_amd.synthetic import make_checkins
+    data = make_checkins(200, 4000, 80, seed=17)
+    m = _model(4000, 32, 32, emb_std=0.01)
+    old = catalog.PAIR_SURV_CAP
+    catalog.PAIR_SURV_CAP = 64
+    try:
+        b = _run(m, data, 60, True)
+        st = m._last_bound_stats.cpu().numpy()
+    finally:
+        catalog.PAIR_SURV_CAP = old
+    assert st[1] > 0, "no user overflowed"
+    _same(b, _run(m, data, 60, False))
