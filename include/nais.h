@@ -283,7 +283,13 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  *                      exactly as nais_pair_gather_topk leaves them (NaNs counted into *nan_count).
  *                      Tables: block b (columns col0 + b*block_cols ..) has hi at tables +
  *                      b*block_stride and lo lo_offset elements further, row pitch ld. stats (may be
- *                      NULL): stats[0] += candidates refined, stats[1] += overflowed users.
+ *                      NULL): stats[0] += candidates refined, stats[1] += overflowed users. tau (may
+ *                      be NULL): per user a threshold key to use when larger than its own k-th lower
+ *                      key -- a column shard of a process group passes the k-th lower key over ALL
+ *                      shards (exchanged after the last block) and then returns only its candidates
+ *                      that can reach the global top-k: kcount may be < k (padding as short lists).
+ *                      A column shard's k-th lower key is a lower bound of the global k-th exact key,
+ *                      so every global winner on this shard is still returned.
  */
 int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
                               int64_t col0, int64_t cols, const int64_t* region_of,
@@ -299,8 +305,9 @@ int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int6
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
                               const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
-                              const int32_t* surv_count, int32_t surv_cap, uint64_t* keys,
-                              int32_t* kcount, int32_t* nan_count, int32_t* stats, void* stream);
+                              const int32_t* surv_count, int32_t surv_cap, const uint64_t* tau,
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* stats,
+                              void* stream);
 /*
  * Power-law prior on the pairs route (powerLaw.py:86-92, run.py:537-539; the direct route's
  * nais_score_topk with a prior computes the same G rows per user):

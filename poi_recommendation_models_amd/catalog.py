@@ -385,7 +385,7 @@ def _masked_streams(dev, table_cus):
 
 def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_mat, stream, force,
                       rows_only=False, cols=None, events=None, prior=None, no_side_streams=False,
-                      group=None, return_keys=False):
+                      group=None, return_keys=False, tau_group=None):
     """Pairs strategy. `cols` = (c0, c1): score only POIs [c0, c1) (top-k ids are global POI ids;
     a column shard of sharding.distributed_topk_pairs). `events`: optional list that receives
     (kind, start, end) HIP events around every table / gather / top-k launch. `prior` = (a, b,
@@ -397,7 +397,13 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
     users one pass can hold), and each user's max G over ITS columns is MAX all-reduced before the
     blend, so every rank normalises by the whole catalog's max (run.py:55-59) -- one [users]
     int64 collective per pass. `return_keys`: also return the f64 blended score of each returned
-    candidate (the merge key of sharding.distributed_topk_pairs)."""
+    candidate (the merge key of sharding.distributed_topk_pairs).
+
+    `tau_group` (a column shard's process group, no prior): on the bounded route every rank takes
+    the route or none does (one MIN all-reduce), and before the refine the ranks exchange their
+    lower-bound lists (sharding.global_kth_keys), so each refines only what can reach the GLOBAL
+    top-k -- the refine then shrinks with the world size like the tables and gathers; the returned
+    lists may be short (padding id -1), which the merge ranks last."""
     dev = model._check_device()
     csr = device_csr(train_matrix, dev)
     P = model._item_tables()[0].shape[0]
@@ -573,6 +579,9 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             # the per-user lower-bound lists and survivor keys
             bnd[0] = bounded_ok and (len(blocks) * 2 * J * ld * 4 + m * (PAIR_SURV_CAP + k) * 8
                                      <= budget)
+            if tau_group is not None and bounded_ok:   # the same route on every rank
+                from .sharding import agree_min
+                bnd[0] = bool(agree_min(int(bnd[0]), dev, tau_group))
             if bnd[0]:
                 arena = torch.empty(len(blocks), 2, J, ld, dtype=torch.int32, device=dev)
                 lokeys = torch.empty(m, k, dtype=torch.int64, device=dev)
@@ -664,12 +673,17 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         t.record_stream(t_)
             if bnd[0]:   # the exact refine of every user's surviving candidates (all CUs)
                 stats = torch.zeros(2, dtype=torch.int32, device=dev)
+                tau_g = None
+                if tau_group is not None:   # the k-th lower key over every rank's columns
+                    from .sharding import global_kth_keys
+                    tau_g = timed("tau_exchange", lambda: global_kth_keys(lokeys, locount, k, tau_group))
                 timed("refine", lambda: _capi.check(lib.nais_pair_refine_topk(
                     arena.data_ptr(), 2 * J * ld, J * ld, ld, W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0_all, NC, float(model.beta), k,
                     lokeys.data_ptr(), locount.data_ptr(), surv.data_ptr(), scount.data_ptr(),
-                    PAIR_SURV_CAP, keys.data_ptr(), kcount.data_ptr(), counters[0:1].data_ptr(),
-                    stats.data_ptr(), st), "nais_pair_refine_topk"))
+                    PAIR_SURV_CAP, tau_g.data_ptr() if tau_g is not None else None, keys.data_ptr(),
+                    kcount.data_ptr(), counters[0:1].data_ptr(), stats.data_ptr(), st),
+                    "nais_pair_refine_topk"))
                 model._last_bound_stats = stats
                 del arena, lokeys, locount, surv, scount
             del tabs

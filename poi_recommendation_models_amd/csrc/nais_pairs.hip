@@ -873,7 +873,8 @@ pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t
                         const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
                         float beta, int k, const unsigned long long* __restrict__ lokeys,
                         const int32_t* __restrict__ locount, const unsigned long long* __restrict__ surv,
-                        const int32_t* __restrict__ scount, int cap, unsigned long long* __restrict__ keys,
+                        const int32_t* __restrict__ scount, int cap,
+                        const unsigned long long* __restrict__ tau_in, unsigned long long* __restrict__ keys,
                         int32_t* __restrict__ kcount, int32_t* __restrict__ nan_count,
                         int32_t* __restrict__ stats) {
   __shared__ unsigned long long lk[GW][RF_LDS];
@@ -885,7 +886,10 @@ pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t
   const int64_t u = users[slot];
   const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
   const int cnt = locount[slot];
-  const unsigned long long tau = cnt == k ? lokeys[slot * k + k - 1] : 0ull;
+  // tau_in: a threshold at least this large, e.g. the k-th lower key over every column shard of a
+  // process group (each shard then refines only what can reach the GLOBAL top-k)
+  unsigned long long tau = cnt == k ? lokeys[slot * k + k - 1] : 0ull;
+  if (tau_in && tau_in[slot] > tau) tau = tau_in[slot];
   const int sc = scount[slot];
   unsigned long long* L = lk[w];
   int nk = 0;             // the running exact list L[0 .. nk)
@@ -1167,8 +1171,9 @@ int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int6
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
                               const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
-                              const int32_t* surv_count, int32_t surv_cap, uint64_t* keys,
-                              int32_t* kcount, int32_t* nan_count, int32_t* stats, void* stream) {
+                              const int32_t* surv_count, int32_t surv_cap, const uint64_t* tau,
+                              uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* stats,
+                              void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || k <= 0 || surv_cap < 64 || block_cols <= 0 ||
       ld < std::min<int64_t>(block_cols, cols) || lo_offset < 0 || block_stride < 0)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
@@ -1183,6 +1188,7 @@ int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int6
                      rowmap, indptr, indices, users, num_users, col0, cols, beta, (int)k,
                      reinterpret_cast<const unsigned long long*>(lo_keys), lo_count,
                      reinterpret_cast<const unsigned long long*>(surv), surv_count, (int)surv_cap,
+                     reinterpret_cast<const unsigned long long*>(tau),
                      reinterpret_cast<unsigned long long*>(keys), kcount, nan_count, stats);
   return nais_internal_check_launch("pair_refine_topk_kernel");
 }

@@ -89,6 +89,25 @@ def all_gather_cat(block, group=None):
     return out
 
 
+_SIGN = -(1 << 63)   # int64 with only the top bit set: u64 keys XOR it order as signed int64
+
+
+def global_kth_keys(lo_keys, lo_count, k, group=None):
+    """The bounded route's threshold over every column shard: per user the k-th largest of all
+    ranks' lower-bound keys (lo_keys [m, k] uint64 bit patterns as int64, lo_count[m] valid, the
+    k best of this rank's columns; nais_pair_bound_topk) -> [m] int64 (u64 bits; 0 where the shards
+    hold fewer than k keys together). One all_gather of the [m, k] lists (8 B per entry, the size of
+    the top-k exchange) and a torch.topk over world * k per user. Every key is a lower bound of a
+    distinct candidate's exact key, so the result bounds the GLOBAL k-th exact key from below
+    (include/nais.h nais_pair_refine_topk `tau`)."""
+    m = lo_keys.shape[0]
+    world = _world(group)
+    valid = torch.arange(k, device=lo_keys.device)[None, :] < lo_count[:, None]
+    mine = torch.where(valid, lo_keys, torch.zeros_like(lo_keys)) ^ _SIGN     # signed order
+    allk = all_gather_cat(mine, group).view(world, m, k).permute(1, 0, 2).reshape(m, world * k)
+    return torch.topk(allk, k, dim=1).values[:, k - 1] ^ _SIGN
+
+
 def column_blocks(num_pois, world):
     """[(c0, c1)] per rank: rank r owns POIs [r*S, (r+1)*S) clipped to P, S = ceil(P / world).
     With P % world != 0 the last block is narrower, and a rank may own no column at all."""
@@ -219,10 +238,12 @@ def distributed_topk_pairs(model, train_matrix, users, k, group=None, events=Non
     out = _score_topk_pairs(model, csr, users, k, kw.get("region_of"), kw.get("coords"),
                             kw.get("latlon_mat"), None, force=True, cols=(c0, c1), events=events,
                             prior=prior, group=grp if prior is not None else None,
-                            return_keys=prior is not None)
+                            return_keys=prior is not None, tau_group=grp if prior is None else None)
     if world == 1:
         return out[0], out[1]
     ids, sc = out[0], out[1]
+    if prior is None:   # a shard's list may be short on the bounded route (global threshold):
+        sc = torch.where(ids >= 0, sc, torch.full_like(sc, float("-inf")))   # padding ranks last
     # the exchange: one all-gather of this rank's [n, k] block per array ([world * n, k], rank
     # order = ascending POI ranges), then the merge over the world * k candidates per user
     mark = _marker(events, dev)

@@ -525,3 +525,55 @@ def test_every_collective_world_n_gloo(tmp_path, world):
     res = _collectives.run(world, "gloo", str(tmp_path / "gloo.npz"))
     names = _collectives.assert_matches_expected(res, world, device_merges=False)
     assert len(names) == 17
+
+
+def _tau_case(rank, k=5, m=7):
+    """Rank r's lower-bound lists: u64 keys (score bits << 32 | ~id) sorted descending, some short."""
+    rng = np.random.default_rng(100 + rank)
+    keys = np.zeros((m, k), dtype=np.uint64)
+    cnt = np.zeros(m, dtype=np.int32)
+    for u in range(m):
+        c = k if u % 3 else rng.integers(0, k + 1)
+        sc = np.sort(rng.random(c).astype(np.float32))[::-1]
+        ids = rng.choice(1000, c, replace=False) + 1000 * rank
+        kk = (sc.view(np.uint32).astype(np.uint64) | np.uint64(0x80000000)) << np.uint64(32)
+        kk |= (np.uint64(0xFFFFFFFF) - ids.astype(np.uint64))
+        keys[u, :c] = np.sort(kk)[::-1]
+        keys[u, c:] = np.uint64(0xDEADBEEFDEADBEEF)   # stale entries past the count are ignored
+        cnt[u] = c
+    return keys, cnt
+
+
+def _worker_tau(rank, world, port, q):
+    import torch.distributed as dist
+    from poi_recommendation_models_amd.sharding import global_kth_keys
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _rccl_calls_only(dist)
+    keys, cnt = _tau_case(rank)
+    tau = global_kth_keys(torch.from_numpy(keys.view(np.int64)), torch.from_numpy(cnt), 5)
+    q.put((rank, tau.numpy().view(np.uint64)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_global_kth_lower_key_world_n(world):
+    """The bounded route's global threshold: per user the k-th largest of every rank's valid
+    lower-bound keys (unsigned order), 0 when the ranks hold fewer than k together."""
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_tau, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    cases = [_tau_case(r) for r in range(world)]
+    for u in range(7):
+        allk = sorted((int(kk) for keys, cnt in cases for kk in keys[u, :cnt[u]]), reverse=True)
+        want = allk[4] if len(allk) >= 5 else 0
+        for _, tau in res:
+            assert int(tau[u]) == want
