@@ -775,7 +775,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        per, nl = {}, {}
+        per, nl, span = {}, {}, {}
         for step_ev in evs:
             ref = next((e0 for _, e0, _, _ in step_ev if e0 is not None), None)
             spans = {}
@@ -785,6 +785,7 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                     continue
                 spans.setdefault(kind, []).append((ref.elapsed_time(e0), ref.elapsed_time(e1)))
                 nl[kind] = nl.get(kind, 0) + launches
+                span.setdefault(kind, []).append(spans[kind][-1][1] - spans[kind][-1][0])
             # busy time of each kind = the union of its launch intervals: the table launches of
             # consecutive blocks overlap (two table streams, catalog.PAIR_TABLE_STREAMS)
             for kind, iv in spans.items():
@@ -795,6 +796,9 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                         end = hi
                 per.setdefault(kind, []).append(busy)
         per["_launches"] = nl
+        # mean span of one launch (its own HIP events, on its own stream): what rocprofv3 reports
+        # as a dispatch's duration, overlap with the other table stream included
+        per["_span_ms"] = {kd: float(np.mean(v)) for kd, v in span.items()}
         return el, per
 
     elapsed, per = run(a.precision, a.warmup, a.steps)
@@ -887,6 +891,11 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
                            % PRODUCTS[precision]),
             "algorithmic_flop_per_step": tflops, "ms_per_step": t_ms, "cus": table_cus,
             "launches_per_step": per["_launches"].get("table", 0) // ns,
+            # achieved = the step's FLOP / the union of the table launches' intervals; a launch's own
+            # span is longer, since consecutive blocks overlap on the two table streams
+            "avg_launch_ms": per.get("_span_ms", {}).get("table"),
+            "busy_ms_per_launch": t_ms / max(1, per["_launches"].get("table", 0) // ns),
+            "table_streams": catalog.PAIR_TABLE_STREAMS,
         }
         return gather, table
 
@@ -896,21 +905,22 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
     # the roofline line is the kernel on the job's critical path (the longer of the two streams)
     dominant = table if (table["ms_per_step"] or 0) > (gather["ms_per_step"] or 0) else gather
     other = gather if dominant is table else table
-    try:
+    try:   # the PMC traffic of both kernels (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, profiles/)
         tj = json.load(open(a.traffic_json))
-        key = ("pairs_gather_topk" if fused else "pairs_gather") if dominant is gather else \
-            "pairs_table_" + a.precision
-        e = tj.get(key, {})
-        ok = (e.get("num_users") == a.num_users and e.get("num_pois") == P and e.get("world") == world
-              and e.get("block_cols") == catalog.PAIR_BLOCK_COLS
-              and e.get("precision", a.precision) == a.precision)
-        dominant["traffic"] = e.get("hbm_bytes_per_launch") if ok else None
-        if ok and dominant is table:
-            dominant["traffic_note"] = "per launch (one 512-column table block)"
+        gkey = ("pairs_bound_topk" if per.get("bounded") else
+                "pairs_gather_topk" if fused else "pairs_gather")
+        for dct, key in ((gather, gkey), (table, "pairs_table_" + a.precision)):
+            e = tj.get(key, {})
+            ok = (e.get("num_users") == a.num_users and e.get("num_pois") == P and e.get("world") == world
+                  and e.get("block_cols") == catalog.PAIR_BLOCK_COLS
+                  and e.get("precision", a.precision) == a.precision)
+            dct["traffic"] = e.get("hbm_bytes_per_launch") if ok else None
+            if ok and dct is table:
+                dct["traffic_note"] = "per launch (one 512-column table block)"
     except Exception:
-        dominant["traffic"] = None
-    if "traffic" not in dominant:
-        dominant["traffic"] = None
+        pass
+    for dct in (gather, table):
+        dct.setdefault("traffic", None)
     dominant["note"] = ("gather: algorithmic bytes per launch (one %d-column stripe) = sum_u h_u x "
                         "columns x %d B table reads + 12 B CSR id + row map per history entry; table: "
                         % (stripes_of(bool(per.get("bounded")))[1], 4 if per.get("bounded") else 8) +

@@ -17,7 +17,7 @@ rows = []
 for sub in ("pmc_fetch", "pmc_write"):
     for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
         n = r["Kernel_Name"]
-        if any(t in n for t in ("pair_gather", "catalog", "topk", "gather_rows")):  # noqa: E501
+        if any(t in n for t in ("pair_gather", "pair_bound", "pair_refine", "catalog", "topk", "gather_rows")):  # noqa: E501
             name = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             rows.append({"kernel": name, "dispatch": r["Dispatch_Id"], "counter": r["Counter_Name"],
                          "value_kb": float(r["Counter_Value"]), "grid": r["Grid_Size"],
@@ -38,6 +38,7 @@ out = {}
 TABLE = {"fp16x6": "catalog_score_x6n_kernel<64, 4, 1, 0>",   # the 16x16x32 form (VAR 0: basic)
          "fp16x3": "catalog_score_x3b_kernel<32, 2, 0, 8, 2>"}
 for tag, key in (("pair_gather_topk", "pairs_gather_topk"), ("pair_gather_kernel", "pairs_gather"),
+                 ("pair_bound_topk", "pairs_bound_topk"), ("pair_refine_topk", "pairs_refine_topk"),
                  (TABLE.get(precision, "catalog"), "pairs_table_" + precision), ("gather_rows", "gather_rows")):
     sel = [r for r in rows if tag in r["kernel"]]
     f = [r["value_kb"] for r in sel if r["counter"] == "FETCH_SIZE"]
