@@ -266,8 +266,9 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  * Bounded gather + exact refine (filter-and-refine top-k; DESIGN.md (d) "bounded gather"): the
  * lists of nais_pair_gather_topk -- the same ids and score bits -- from half the gathered bytes.
  *   nais_pair_table_split  nais_pair_table's pairs stored split16: hi[r*ld + c-col0] = (top 16 bits
- *                      of e*s) << 16 | (top 16 bits of e), lo[...] = the low 16 bits likewise; hi
- *                      alone holds both values truncated to 8 significant bits, hi + lo the fp32 bits.
+ *                      of e*s) << 16 | (top 16 bits of e) -- both values truncated to 8 significant
+ *                      bits -- and ex[2*(r*ld + c-col0)] = e, ex[... + 1] = e*s (the exact pair,
+ *                      8 bytes side by side; ex row pitch 2*ld).
  *   nais_pair_bound_topk   per column block (stream-ordered over the blocks of one user list): each
  *                      user's S, N = sum over its history of the truncated e, e*s and sum |e*s| give
  *                      an interval around every candidate's exact score (the fp32 arithmetic of
@@ -278,11 +279,11 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  *                      zero it before the first block; compacted when full, -1 if it overflows).
  *                      Keys as nais_pair_gather_topk. ld % 4 == 0, hi 16-byte aligned, k <= 256.
  *   nais_pair_refine_topk  after the last block: for each survivor whose upper key reaches the final
- *                      k-th lower key (every column for an overflowed user), the exact N, S from
- *                      hi + lo in history (CSR) order and its score; keys / kcount receive the top-k
+ *                      k-th lower key (every column for an overflowed user), the exact N, S from the
+ *                      ex pairs in history (CSR) order and its score; keys / kcount receive the top-k
  *                      exactly as nais_pair_gather_topk leaves them (NaNs counted into *nan_count).
- *                      Tables: block b (columns col0 + b*block_cols ..) has hi at tables +
- *                      b*block_stride and lo lo_offset elements further, row pitch ld. stats (may be
+ *                      ex: block b (columns col0 + b*block_cols ..) at ex + b*block_stride (uint32
+ *                      words, even), rows of ld pairs (nais_pair_table_split's ex). stats (may be
  *                      NULL): stats[0] += candidates refined, stats[1] += overflowed users. tau (may
  *                      be NULL): per user a threshold key to use when larger than its own k-th lower
  *                      key -- a column shard of a process group passes the k-th lower key over ALL
@@ -294,13 +295,13 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
 int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
                               int64_t col0, int64_t cols, const int64_t* region_of,
                               const double* coords, const double* latlon_mat, uint32_t* hi,
-                              uint32_t* lo, int64_t ld, int32_t* work, void* stream);
+                              uint32_t* ex, int64_t ld, int32_t* work, void* stream);
 int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowmap,
                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
                              uint64_t* lo_keys, int32_t* lo_count, uint64_t* surv, int32_t* surv_count,
                              int32_t surv_cap, int32_t* work, void* stream);
-int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int64_t lo_offset,
+int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                               int64_t ld, int64_t block_cols, const int32_t* rowmap,
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,

@@ -231,7 +231,7 @@ def load(path: str | None = None):
     lib.nais_pair_bound_topk.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp, vp,
                                          i32, vp, vp]
     lib.nais_pair_refine_topk.restype = i32
-    lib.nais_pair_refine_topk.argtypes = [vp, i64, i64, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32,
+    lib.nais_pair_refine_topk.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32,
                                           vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32
     lib.nais_stream_create_cu_mask.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]

@@ -269,7 +269,7 @@ PAIR_SPLIT_STEP = 8
 # from split16 tables -- the gather streams only their hi halves (4 bytes per history entry and
 # candidate instead of 8), keeps per user the k best LOWER bounds of the exact scores and the
 # candidates whose UPPER bound reaches the k-th of them, and a refine pass recomputes those
-# candidates' exact sums from hi + lo in CSR order: the same lists, ids and score bits as the exact
+# candidates' exact sums from their (e, e*s) pairs in CSR order: the same lists, ids and score bits as the exact
 # fused gather (tests/test_gpu_bounded.py compares every user). Every block's tables stay resident
 # until the refine (J x P x 8 bytes: 80 GB at config 4), so the route is taken only when they fit
 # the memory budget; otherwise the exact fused gather runs on double-buffered tables.
@@ -492,7 +492,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
         return wq_of[h]
 
     def table(tab, c0, w, stream_):
-        if tab.dtype == torch.int32:   # the bounded route's split16 tables
+        if isinstance(tab, tuple):   # the bounded route's split16 tables (hi words, ex pairs)
             _capi.check(lib.nais_pair_table_split(prm, items.data_ptr(), J, c0, w, _capi.ptr(reg),
                                                   _capi.ptr(cor), _capi.ptr(llm), tab[0].data_ptr(),
                                                   tab[1].data_ptr(), ld, wq(stream_), stream_),
@@ -577,13 +577,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             blocks = list(range(c0_all, c1_all, W))
             # bounded route: every block's split16 tables (2 x J x ld words each) resident, plus
             # the per-user lower-bound lists and survivor keys
-            bnd[0] = bounded_ok and (len(blocks) * 2 * J * ld * 4 + m * (PAIR_SURV_CAP + k) * 8
+            bnd[0] = bounded_ok and (len(blocks) * 3 * J * ld * 4 + m * (PAIR_SURV_CAP + k) * 8
                                      <= budget)
             if tau_group is not None and bounded_ok:   # the same route on every rank
                 from .sharding import agree_min
                 bnd[0] = bool(agree_min(int(bnd[0]), dev, tau_group))
-            if bnd[0]:
-                arena = torch.empty(len(blocks), 2, J, ld, dtype=torch.int32, device=dev)
+            if bnd[0]:   # per block: the hi words [J, ld] and the exact (e, e*s) pairs [J, 2 ld]
+                arena = (torch.empty(len(blocks), J, ld, dtype=torch.int32, device=dev),
+                         torch.empty(len(blocks), J, 2 * ld, dtype=torch.int32, device=dev))
                 lokeys = torch.empty(m, k, dtype=torch.int64, device=dev)
                 locount = torch.zeros(m, dtype=torch.int32, device=dev)
                 surv = torch.empty(m, PAIR_SURV_CAP, dtype=torch.int64, device=dev)
@@ -613,7 +614,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 first_all = PAIR_FIRST_TABLE_ALL_CUS
                 if first_all:      # block 0's table alone, on the caller's stream (all CUs)
                     w0 = min(W, c1_all - blocks[0])
-                    tab0 = arena[0] if bnd[0] else tabs[0]
+                    tab0 = (arena[0][0], arena[1][0]) if bnd[0] else tabs[0]
                     timed("table", lambda: table(tab0, blocks[0], w0, st))
                 for t_ in tss:
                     t_.wait_stream(torch_stream)
@@ -632,7 +633,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     events.append(("gather_share", None, None, share))
             for b, c0 in enumerate(blocks):
                 w = min(W, c1_all - c0)
-                tab = arena[b] if bnd[0] else tabs[b % len(tabs)]
+                tab = (arena[0][b], arena[1][b]) if bnd[0] else tabs[b % len(tabs)]
                 if overlap:
                     tsb = tss[b % len(tss)]
                     if done_g[b % 2] is not None and not bnd[0]:
@@ -668,7 +669,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 for t_ in tss:
                     torch_stream.wait_stream(t_)
                 for t in [*tabs, *pr_of.values(), *([wq_slots] if wq_slots is not None else []),
-                          *((arena, lokeys, locount, surv, scount) if bnd[0] else ())]:
+                          *((*arena, lokeys, locount, surv, scount) if bnd[0] else ())]:
                     for t_ in (*tss, gs):   # not handed to the main stream early
                         t.record_stream(t_)
             if bnd[0]:   # the exact refine of every user's surviving candidates (all CUs)
@@ -678,7 +679,7 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     from .sharding import global_kth_keys
                     tau_g = timed("tau_exchange", lambda: global_kth_keys(lokeys, locount, k, tau_group))
                 timed("refine", lambda: _capi.check(lib.nais_pair_refine_topk(
-                    arena.data_ptr(), 2 * J * ld, J * ld, ld, W, rowmap.data_ptr(), csr.indptr.data_ptr(),
+                    arena[1].data_ptr(), 2 * J * ld, ld, W, rowmap.data_ptr(), csr.indptr.data_ptr(),
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0_all, NC, float(model.beta), k,
                     lokeys.data_ptr(), locount.data_ptr(), surv.data_ptr(), scount.data_ptr(),
                     PAIR_SURV_CAP, tau_g.data_ptr() if tau_g is not None else None, keys.data_ptr(),

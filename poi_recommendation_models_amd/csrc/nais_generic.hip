@@ -91,7 +91,8 @@ struct CatArgs {
   float* e;                 // table: e / es [row][ld] (e != nullptr selects the table mode)
   float* es;
   int64_t ld, col0, cols, nitems;
-  uint32_t sel_e, sel_es;   // the table words (float or split16, nais_internal.h)
+  uint32_t sel_e;           // the e words (float or the split16 hi, nais_internal.h)
+  int32_t ex;               // split16: es holds (e, e*s) pairs, row pitch 2 * ld
 };
 
 struct CatLds {
@@ -217,7 +218,8 @@ __global__ void __launch_bounds__(GX_NT, 1) gx_catalog_kernel(GxP p, CatArgs a) 
           const int64_t o2 = (hbeg + n) * a.ld + (c - a.col0);
           const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(e * st);
           a.e[o2] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, a.sel_e));
-          a.es[o2] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, a.sel_es));
+          if (a.ex) reinterpret_cast<float2*>(a.es)[o2] = make_float2(e, e * st);
+          else a.es[o2] = e * st;
         }
       } else {
         S[t] += gx::half_sum32(e);
@@ -421,7 +423,7 @@ int nais_gx_catalog(const nais_params_t* params, const int64_t* indptr, const in
   a.score_ld = score_ld;
   a.nan_count = nan_count;
   a.sel_e = split ? NAIS_SEL_HI : NAIS_SEL_E;
-  a.sel_es = split ? NAIS_SEL_LO : NAIS_SEL_ES;
+  a.ex = split ? 1 : 0;
   auto kern = dist ? gx_catalog_kernel<true> : gx_catalog_kernel<false>;
   if (!e) {   // catalog rows: grid (candidate tiles, users)
     a.indices = indices;
@@ -439,7 +441,7 @@ int nais_gx_catalog(const nais_params_t* params, const int64_t* indptr, const in
     a.indices = items + base;
     a.nitems = std::min<int64_t>(nitems - base, int64_t(65535) * 32);
     a.e = e + base * ld;
-    a.es = es + base * ld;
+    a.es = es + base * ld * (split ? 2 : 1);
     dim3 grid((unsigned)((cols + GX_TT - 1) / GX_TT), (unsigned)((a.nitems + 31) / 32));
     hipLaunchKernelGGL(kern, grid, dim3(GX_NT), lds, st, p, a);
     if ((rc = nais_internal_check_launch("gx_catalog_kernel (table)"))) return rc;

@@ -30,12 +30,11 @@ __attribute__((visibility("hidden"))) int nais_gx_forward(
     const float* latlon, int64_t ll_ld, float* out, int32_t* nan_count, int32_t flags, hipStream_t st);
 
 // Table words (v_perm_b32 selectors over {S0 = bits of e*s, S1 = bits of e}). The float tables
-// store e and e*s as they are; the split16 tables (nais_pair_table_split) store
-//   hi = [top 16 bits of e*s | top 16 bits of e]   lo = [low 16 bits of e*s | low 16 bits of e]
+// store e and e*s as they are (NAIS_SEL_E); the split16 form (nais_pair_table_split) stores
+//   hi = [top 16 bits of e*s | top 16 bits of e]  (NAIS_SEL_HI)  and  ex = (e, e*s) side by side,
 // so hi alone gives both values truncated to 8 significant bits (relative error < 2^-7, toward
-// zero; the bounded gather's phase 1) and hi + lo the exact fp32 bits (its refine).
-constexpr uint32_t NAIS_SEL_E = 0x03020100u, NAIS_SEL_ES = 0x07060504u;
-constexpr uint32_t NAIS_SEL_HI = 0x07060302u, NAIS_SEL_LO = 0x05040100u;
+// zero; the bounded gather's phase 1) and one 8-byte ex read the exact pair (its refine).
+constexpr uint32_t NAIS_SEL_E = 0x03020100u, NAIS_SEL_HI = 0x07060302u;
 
 // ReLU that keeps NaN, as torch.relu (model.py:71): fmaxf / v_max_f32 would return 0 for a NaN.
 __device__ __forceinline__ float nais_relu(float v) { return (v < 0.f) ? 0.f : v; }

@@ -74,16 +74,21 @@ struct TableOut {
   // work queue (x6n only): the launch's item counter, zeroed before it, and the item grid it covers
   int32_t* work = nullptr;
   int32_t ngroups = 0, ntiles = 0;
-  // the words written to e / es (nais_internal.h): the float tables (e, e*s) or the split16
-  // tables (hi, lo) -- one v_perm_b32 per word, no branch
-  uint32_t sel_e = NAIS_SEL_E, sel_es = NAIS_SEL_ES;
+  // the split16 form (nais_internal.h): e receives the hi words (sel_e = NAIS_SEL_HI, one
+  // v_perm_b32), es the exact (e, e*s) pairs with row pitch 2 * ld (ex = 1)
+  uint32_t sel_e = NAIS_SEL_E;
+  int32_t ex = 0;
 };
 // the pair's two terms for item row `row` (relative to the launch's base) and column offset x
 __device__ __forceinline__ void tab_put(const TableOut& t, int64_t row, int64_t x, float e, float es) {
   const int64_t o = row * t.ld + x;
   const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(es);
   t.e[o] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, t.sel_e));
-  t.es[o] = __uint_as_float(__builtin_amdgcn_perm(sb, eb, t.sel_es));
+  if (t.ex) {
+    reinterpret_cast<float2*>(t.es)[o] = make_float2(e, es);
+  } else {
+    t.es[o] = es;
+  }
 }
 
 // Catalog grid: one workgroup per (user slot, 256-POI tile), user-major dispatch order
@@ -1762,6 +1767,7 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
   // selects, and the table rows are written by buffer stores whose offset is out of range (the
   // store dropped) for the lanes that do not write -- so the tail stays in the step's basic block.
   const uint32_t tab_bytes = tab.e ? (uint32_t)(tab.cols * 4) : 0u;
+  const int exs = tab.ex ? 2 : 1;   // the es / ex row pitch in units of ld
   auto tail = [&](int pj, float p0, float p1, bool live) __attribute__((always_inline)) {
     const auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
     const float q = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);   // groups {g, g + 2}
@@ -1776,15 +1782,17 @@ catalog_score_x6n_kernel(DevParams p, const int64_t* __restrict__ indptr,
     const int64_t row = (hbeg + j0 + pj) * tab.ld;
     const int off = (live && vout) ? (int)(cout - tab.col0) * 4 : (int)0x80000000;
     const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(tab.e + row, (short)0, tab_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tab.es + row, (short)0, tab_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tab.es + row * exs, (short)0, tab_bytes * exs, 0x00020000);
     const bool odd = grp & 1;
     // (the stores as non-temporal or sc1 instead of the default policy, so that the table block
     // being written would not evict the stripe the gather reads from the Infinity Cache: config-4
     // job 0.5968 / 0.5967 / 0.5966 s, base / nt / sc1 means of three interleaved runs, profiles/r5/nt)
-    // (split16 tables: the hi / lo words of the pair, nais_internal.h; one v_perm_b32 each)
+    // Float tables: even lanes e, odd lanes e*s. Split16: even lanes the hi word (one v_perm_b32)
+    // and e into the ex pair, odd lanes e*s into the pair's second word.
     const uint32_t eb = __float_as_uint(e), sb = __float_as_uint(e * sv);
+    const int off2 = tab.ex ? (off < 0 ? off : 2 * off + (odd ? 4 : 0)) : (odd ? off : (int)0x80000000);
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(sb, eb, tab.sel_e), re, odd ? (int)0x80000000 : off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(sb, eb, tab.sel_es), rs, odd ? off : (int)0x80000000, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(odd ? sb : eb, rs, off2, 0, 0);
   };
 
   // One unit per step, in block-major order: block m (16 hidden units) takes its KS groups of 12
@@ -3116,7 +3124,7 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
   TableOut tab;
   if (split) {
     tab.sel_e = NAIS_SEL_HI;
-    tab.sel_es = NAIS_SEL_LO;
+    tab.ex = 1;
   }
   tab.ld = ld;
   tab.cols = cols;
@@ -3127,7 +3135,7 @@ int32_t pair_table_impl(const nais_params_t* params, const int64_t* items, int64
     const int64_t base = g0 * tab.gi;
     tab.nitems = std::min<int64_t>(num_items - base, groups_per_launch * tab.gi);
     tab.e = e + base * ld;
-    tab.es = es + base * ld;
+    tab.es = es + base * ld * (split ? 2 : 1);
     tab.col0 = col0;
     const int ng = (int)((tab.nitems + tab.gi - 1) / tab.gi);
     if (params->precision == NAIS_PRECISION_FP32)
@@ -3157,9 +3165,9 @@ int32_t nais_pair_table(const nais_params_t* params, const int64_t* items, int64
 int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
                               int64_t col0, int64_t cols, const int64_t* region_of,
                               const double* coords, const double* latlon_mat, uint32_t* hi,
-                              uint32_t* lo, int64_t ld, int32_t* work, void* stream) {
+                              uint32_t* ex, int64_t ld, int32_t* work, void* stream) {
   return pair_table_impl(params, items, num_items, col0, cols, region_of, coords, latlon_mat,
-                         reinterpret_cast<float*>(hi), reinterpret_cast<float*>(lo), ld, work, stream,
+                         reinterpret_cast<float*>(hi), reinterpret_cast<float*>(ex), ld, work, stream,
                          true);
 }
 

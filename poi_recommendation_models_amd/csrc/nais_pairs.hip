@@ -518,7 +518,7 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
 // ---------------------------------------------------------------------------------------------
 // Bounded gather + exact refine: the fused top-k of pair_gather_topk_kernel from half its bytes.
 // The tables are split16 (nais_pair_table_split, nais_internal.h): hi[r, c] = the top 16 bits of
-// e and of e*s, lo[r, c] = their low 16 bits. Phase 1 (pair_bound_topk_kernel, one launch per
+// e and of e*s, ex[r, c] = the exact (e, e*s) pair. Phase 1 (pair_bound_topk_kernel, one launch per
 // column block) streams only the hi rows -- 4 bytes per (user, history item, candidate) instead
 // of 8 -- and sums, per candidate, S^ = sum e^, N^ = sum es~ and A^ = sum |es~| of the truncated
 // values (e^ <= e < e^ (1 + 2^-7); |e*s - es~| < 2^-7 |es~|, see bound_rows), which bound the
@@ -534,14 +534,13 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
 // the k-th exact key >= the final tau (k candidates have exact key >= their lower bound >= tau),
 // so its upper bound reaches every tau on the way: it is a survivor. Phase 2
 // (pair_refine_topk_kernel) recomputes, for each survivor with upper key >= the final tau, the
-// exact Na and Sa from hi + lo in history (CSR) order -- the exact gather's operations on the
-// same fp32 bits -- and ranks them: the same top-k lists, ids and score bits, as the exact gather.
+// exact Na and Sa in history (CSR) order -- the exact gather's operations on the
+// same fp32 bits, read as one (e, e*s) pair per row from the ex table -- and ranks them: the same
+// top-k lists, ids and score bits, as the exact gather.
 // Keys as pair_gather_topk_kernel: ordered(score) << 32 | (0xFFFFFFFF - poi).
 constexpr int BCPL = 8;                       // columns per lane: 32-byte hi rows per lane
 constexpr int BSTRIPE = 64 * BCPL;            // 512 columns per wave (one launch per block)
 constexpr int BK_LDS = 512;                   // keys per wave in LDS: k + 256 offered (k <= 256)
-constexpr uint32_t SEL_REC_E = 0x05040100u;   // perm(hi, lo): [hi.lo16 | lo.lo16] = bits of e
-constexpr uint32_t SEL_REC_ES = 0x07060302u;  // perm(hi, lo): [hi.hi16 | lo.hi16] = bits of e*s
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -859,15 +858,15 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
 }
 
 // Phase 2: per user, the exact scores of the candidates whose upper key reaches the final tau (all
-// columns of [col0, col0 + cols) for an overflowed user), from hi + lo of the block tables
-//   tables + b * bstride + row * ld + x  (hi),  + lo_off (lo),  column col0 + b * bcols + x,
+// columns of [col0, col0 + cols) for an overflowed user), from the ex pairs of the block tables
+//   X + b * bstride + row * ld + x  (uint2 pairs),  column col0 + b * bcols + x,
 // summed in history (CSR) order as pair_gather_topk_kernel sums them, 64 candidates (one per lane)
 // at a time; a running top-k in LDS. stats[0] += candidates refined, stats[1] += overflowed users.
 constexpr int RF_LDS = 512;   // running list (k <= 256) + 64 offered, padded to a power of two
 constexpr int RF_CAND = 512;  // kept survivors sorted in LDS (more: streamed unsorted)
 
 __global__ void __launch_bounds__(GW * 64)
-pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t lo_off, int64_t ld,
+pair_refine_topk_kernel(const uint2* __restrict__ X, int64_t bstride, int64_t ld,
                         int64_t bcols, const int32_t* __restrict__ rowmap,
                         const int64_t* __restrict__ indptr, const int64_t* __restrict__ indices,
                         const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
@@ -898,7 +897,7 @@ pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t
   auto batch = [&](int64_t r, bool valid) __attribute__((always_inline)) {
     const int64_t rr = valid ? r : 0;                   // invalid lanes read a column that exists
     const int64_t b = rr / bcols;
-    const int64_t xo = b * bstride + (rr - b * bcols);
+    const int64_t xo = b * bstride + (rr - b * bcols);  // in (e, e*s) pairs
     const int64_t c = col0 + rr;
     float Sa = 0.f, Na = 0.f;
     bool in_hist = false;
@@ -907,33 +906,30 @@ pair_refine_topk_kernel(const uint32_t* __restrict__ T, int64_t bstride, int64_t
       int64_t mine = 0, mid = -1;
       if (lane < jn) {
         mid = indices[hb + j0 + lane];
-        mine = int64_t(rowmap[mid]) * ld;
+        mine = int64_t(rowmap[mid]) * ld;   // ex rows hold ld pairs
       }
       const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
       const uint32_t ilo = uint32_t(mid), ihi = uint32_t(mid >> 32);
       int jj = 0;
       for (; jj + GU <= jn; jj += GU) {
-        uint32_t h[GU], l[GU];
+        uint2 v[GU];
         int64_t id[GU];
 #pragma unroll
         for (int g = 0; g < GU; ++g) {
-          const int64_t o = bcast64(mlo, mhi, jj + g) + xo;
           id[g] = bcast64(ilo, ihi, jj + g);
-          h[g] = T[o];
-          l[g] = T[o + lo_off];
+          v[g] = X[bcast64(mlo, mhi, jj + g) + xo];   // one 8-byte read: one line per pair
         }
 #pragma unroll
         for (int g = 0; g < GU; ++g) {
-          Sa += __uint_as_float(__builtin_amdgcn_perm(h[g], l[g], SEL_REC_E));
-          Na += __uint_as_float(__builtin_amdgcn_perm(h[g], l[g], SEL_REC_ES));
+          Sa += __uint_as_float(v[g].x);
+          Na += __uint_as_float(v[g].y);
           in_hist |= id[g] == c;
         }
       }
       for (; jj < jn; ++jj) {
-        const int64_t o = bcast64(mlo, mhi, jj) + xo;
-        const uint32_t h = T[o], l = T[o + lo_off];
-        Sa += __uint_as_float(__builtin_amdgcn_perm(h, l, SEL_REC_E));
-        Na += __uint_as_float(__builtin_amdgcn_perm(h, l, SEL_REC_ES));
+        const uint2 v = X[bcast64(mlo, mhi, jj) + xo];
+        Sa += __uint_as_float(v.x);
+        Na += __uint_as_float(v.y);
         in_hist |= bcast64(ilo, ihi, jj) == c;
       }
     }
@@ -1166,7 +1162,7 @@ int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowm
   return NAIS_OK;
 }
 
-int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int64_t lo_offset,
+int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                               int64_t ld, int64_t block_cols, const int32_t* rowmap,
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
                               int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
@@ -1175,16 +1171,17 @@ int32_t nais_pair_refine_topk(const uint32_t* tables, int64_t block_stride, int6
                               uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* stats,
                               void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || k <= 0 || surv_cap < 64 || block_cols <= 0 ||
-      ld < std::min<int64_t>(block_cols, cols) || lo_offset < 0 || block_stride < 0)
+      ld < std::min<int64_t>(block_cols, cols) || block_stride < 0 || block_stride % 2 != 0)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
   if (k > RF_LDS - 256) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
   if (col0 + cols > 0xFFFFFFFFll) return nais_internal_fail(NAIS_E_UNSUPPORTED, "POI ids must fit 32 bits");
   if (num_users == 0) return NAIS_OK;
   if (!rowmap || !indptr || !indices || !users || !lo_keys || !lo_count || !surv || !surv_count ||
-      !keys || !kcount || (cols > 0 && !tables))
+      !keys || !kcount || (cols > 0 && !ex))
     return nais_internal_fail(NAIS_E_INVALID, "missing pointer");
   hipLaunchKernelGGL(pair_refine_topk_kernel, dim3((unsigned)((num_users + GW - 1) / GW)), dim3(GW * 64), 0,
-                     reinterpret_cast<hipStream_t>(stream), tables, block_stride, lo_offset, ld, block_cols,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint2*>(ex), block_stride / 2, ld,
+                     block_cols,
                      rowmap, indptr, indices, users, num_users, col0, cols, beta, (int)k,
                      reinterpret_cast<const unsigned long long*>(lo_keys), lo_count,
                      reinterpret_cast<const unsigned long long*>(surv), surv_count, (int)surv_cap,

@@ -2,7 +2,8 @@
 nais_pair_table_split / nais_pair_bound_topk / nais_pair_refine_topk) returns the exact fused
 gather's top-k -- the same ids and the same score bits -- for every user.
 
-The split16 tables hold the float tables' bits (hi + lo), checked per table kernel; the bounded
+The split16 tables hold the float tables' bits (the hi words' halves, the exact ex pairs), checked
+per table kernel; the bounded
 route is then compared with the exact route (PAIR_BOUNDED off: nais_pair_gather_topk on the float
 tables) on whole jobs, including the shapes that stress the bounds: score clusters (the
 reference's N(0, 0.01) init puts every score near sigmoid(0)), saturated scores (ties at 1.0f broken
@@ -75,19 +76,21 @@ def test_split_tables_hold_the_float_bits(variant, precision, D, H):
     for c0 in (0, 700, P - 200):
         w = min(W, P - c0)
         f = torch.zeros(2, J, W, dtype=torch.float32, device=DEV)
-        t = torch.zeros(2, J, W, dtype=torch.int32, device=DEV)
+        t = torch.zeros(J, W, dtype=torch.int32, device=DEV)       # hi words
+        x = torch.zeros(J, 2 * W, dtype=torch.int32, device=DEV)   # exact (e, e*s) pairs
         _capi.check(lib.nais_pair_table(prm, items.data_ptr(), J, c0, w, _capi.ptr(side[0]), _capi.ptr(side[1]),
                                         None, f[0].data_ptr(), f[1].data_ptr(), W, None, None), "table")
         _capi.check(lib.nais_pair_table_split(prm, items.data_ptr(), J, c0, w, _capi.ptr(side[0]),
-                                              _capi.ptr(side[1]), None, t[0].data_ptr(), t[1].data_ptr(), W,
+                                              _capi.ptr(side[1]), None, t.data_ptr(), x.data_ptr(), W,
                                               None, None), "table_split")
         torch.cuda.synchronize()
         fb = f.cpu().numpy().view(np.uint32)
-        hi, lo = (x.astype(np.uint32) for x in t.cpu().numpy().view(np.uint32))
-        e = (hi << 16) | (lo & 0xFFFF)
-        es = (hi & 0xFFFF0000) | (lo >> 16)
-        np.testing.assert_array_equal(e[:, :w], fb[0][:, :w])
-        np.testing.assert_array_equal(es[:, :w], fb[1][:, :w])
+        hi = t.cpu().numpy().view(np.uint32)
+        ex = x.cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(ex[:, 0:2 * w:2], fb[0][:, :w])        # e
+        np.testing.assert_array_equal(ex[:, 1:2 * w:2], fb[1][:, :w])        # e*s
+        np.testing.assert_array_equal(hi[:, :w] << 16, fb[0][:, :w] & 0xFFFF0000)   # e's top half
+        np.testing.assert_array_equal(hi[:, :w] & 0xFFFF0000, fb[1][:, :w] & 0xFFFF0000)
 
 
 @pytest.mark.parametrize("case", ["bench_like", "reference_init", "beta07", "k1_k256", "region_distance",
