@@ -325,9 +325,17 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     # 1.64 TB/s on 32 CUs)
     per_cu = 72e9 if block_bytes is None or block_bytes <= 512e6 else 51e9
     if gather_bytes == 4:
-        # the bounded gather (hi words, 4 B per entry and column): 65 GB/s per CU measured at 64 and
-        # 80 gather CUs (config 4, round 6: 485.8 / 389.3 ms for 2.02 TB; profiles/r6/bounded)
-        per_cu = 65e9
+        # the bounded gather (hi words, 4 B per entry and column): 65-66 GB/s per CU measured at 64,
+        # 68 and 80 gather CUs (config 4, round 6: 485.8 / 448.6 / 389.3 ms for 2.02 TB;
+        # profiles/r6/bounded, split_ab), and 4-CU steps: 188 / 68 ran 471.4 ms against 476.9 /
+        # 480.2 at 184 / 72 and 490.8 at 180 / 76 on one box (profiles/r6/split_ab)
+        per_cu = 66e9
+        if block_bytes is not None and block_bytes / 2 <= 128e6:
+            # a hi stripe of half the Infinity Cache or less (config 2: 102 MB) is served faster:
+            # 95 GB/s per CU measured at 24 gather CUs (87.5 ms for 0.2 TB, profiles/r6/split_ab)
+            per_cu = 95e9
+        if x6n:
+            step = 4
     cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
