@@ -897,6 +897,14 @@ def bench_pairs(a, model, csr, data, hist_len, p_host, dev, rank, world, dist):
             "busy_ms_per_launch": t_ms / max(1, per["_launches"].get("table", 0) // ns),
             "table_streams": catalog.PAIR_TABLE_STREAMS,
         }
+        nlt = max(1, per["_launches"].get("table", 0) // ns)
+        if table["avg_launch_ms"]:
+            # the literal per-launch rate (FLOP of one launch / its own span): with two table
+            # streams each launch shares its span with the other stream's, so the kernel's
+            # throughput (`achieved`) is ~streams x this
+            table["achieved_per_launch_span"] = tflops / nlt / (table["avg_launch_ms"] * 1e-3) / 1e12
+            table["achieved_basis"] = ("achieved = FLOP per step / the union of the table launches' "
+                                       "intervals (HIP events on both table streams)")
         return gather, table
 
     a_steps = {a.precision: a.steps}
