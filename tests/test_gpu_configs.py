@@ -307,3 +307,53 @@ def test_config4_bench_job_every_user_vs_torch_restatement(config4_job):
     print(f"config 4, all {U} users vs the torch restatement on the device: max |winner score diff| "
           f"{worst_w:.3g}; {ties} sampled candidates above the weakest winner, all within "
           f"{TIE_ULPS} ulps (max excess {worst_over:.3g})")
+
+
+def test_config4_bench_job_every_user_full_catalog(config4_job):
+    """Every one of the bench job's 50,000 users against EVERY candidate of the catalog (not a
+    sample): tests/_torch_pairs.py forms the reference's e and e*s for all 10^10 (history POI,
+    candidate) pairs in torch fp32 ops on the device (rocBLAS GEMMs, a sparse CSR product for the
+    per-user sums -- none of this package's kernels), keeps each user's top-60 over the whole
+    catalog and scores the job's own winners. Asserted: the winners' checker scores within
+    SCORE_ATOL of the job's, and no candidate anywhere beats a user's weakest winner by more than
+    the 4-ulp tie allowance. The checker is pinned to the numpy oracle by
+    tests/test_torch_pairs_checker.py."""
+    from _torch_pairs import check_against_full_catalog, full_catalog_topk
+    data, p, m, csr, ids_p, sc_p = config4_job
+    ti, tv, at = full_catalog_topk(p, data.indptr, data.indices, data.num_pois, 60, ids_p, DEV)
+    dw, same, over = check_against_full_catalog(ids_p, sc_p, ti, tv, at, SCORE_ATOL, TIE_ULPS)
+    print(f"config 4, all {data.num_users} users x all {data.num_pois} POIs vs the torch pairs checker: "
+          f"max |winner score diff| {dw:.3g}; {same} users' top-50 equal the checker's as sets; "
+          f"largest excess of a non-winner over the weakest winner {over:.3g} (allowed: {TIE_ULPS} ulps)")
+
+
+def test_config4_region_distance_job_every_user_full_catalog():
+    """The bench's region_distance leg (north_star's variant: bench.py rd_job -- same users and
+    POIs, 1,024 regions, the POI coordinates) through the pairs route, every user against every
+    candidate of the catalog with the torch pairs checker's region_distance form (model.py:246-297:
+    [E | region] rows, sigmoid(dist_layer(100 |ll|)) features), as the test above."""
+    from _torch_pairs import check_against_full_catalog, full_catalog_topk
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    from poi_recommendation_models_amd.model import NAIS_region_distance_Embedding
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    U, P, D, H, K = 50_000, 100_000, 64, 64, 50
+    data = make_checkins(U, P, 200, seed=2024)                   # bench.py's workload
+    p = init_nais_params(P, D, H, seed=11, emb_std=0.3, bias_std=0.1, variant="region_distance",
+                         num_regions=1024)
+    m = NAIS_region_distance_Embedding(P, D, H, 0.5, 1024, 1)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()}, strict=False)
+    m.report_nan = False
+    m = m.to(DEV).eval()
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    ev = []
+    ids, sc = _score_topk_pairs(m, csr, np.arange(U), K, data.region_of, data.place_coords, None, None,
+                                force=True, events=ev)
+    assert any(kind == "bounded" for kind, *_ in ev)
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    del m
+    ti, tv, at = full_catalog_topk(p, data.indptr, data.indices, P, 60, ids, DEV,
+                                   region_of=data.region_of, coords=data.place_coords)
+    dw, same, over = check_against_full_catalog(ids, sc, ti, tv, at, SCORE_ATOL, TIE_ULPS)
+    print(f"config 4 region_distance, all {U} users x all {P} POIs vs the torch pairs checker: max "
+          f"|winner score diff| {dw:.3g}; {same} users' top-50 equal the checker's as sets; largest "
+          f"excess of a non-winner over the weakest winner {over:.3g} (allowed: {TIE_ULPS} ulps)")
