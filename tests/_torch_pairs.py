@@ -42,8 +42,12 @@ def full_catalog_topk(p, indptr, indices, num_pois, keep, probe_ids, device, bet
     U = len(indptr) - 1
     crow = torch.as_tensor(np.asarray(indptr, np.int64), device=device)
     col = torch.as_tensor(np.asarray(indices, np.int64), device=device)
-    A = torch.sparse_csr_tensor(crow, col, torch.ones(col.numel(), dtype=torch.float32, device=device),
-                                size=(U, P))
+    # the e / e*s rows of the distinct history POIs only (all of them at config 4; a few thousand
+    # of config 5's 10^6)
+    rows, rcol = torch.unique(col, return_inverse=True)
+    J = rows.numel()
+    A = torch.sparse_csr_tensor(crow, rcol, torch.ones(col.numel(), dtype=torch.float32, device=device),
+                                size=(U, J))
     row_of = torch.repeat_interleave(torch.arange(U, device=device), crow[1:] - crow[:-1])
     by_col = torch.argsort(col)
     col_sorted = col[by_col]
@@ -54,22 +58,23 @@ def full_catalog_topk(p, indptr, indices, num_pois, keep, probe_ids, device, bet
     for c0 in range(0, P, block):
         c1 = min(P, c0 + block)
         t = et[c0:c1]                                                  # [w, D]
-        E = torch.empty(P, c1 - c0, dtype=torch.float32, device=device)
+        E = torch.empty(J, c1 - c0, dtype=torch.float32, device=device)
         ES = torch.empty_like(E)
-        for j0 in range(0, P, jchunk):
-            j1 = min(P, j0 + jchunk)
-            h = eh[j0:j1]
+        for j0 in range(0, J, jchunk):
+            j1 = min(J, j0 + jchunk)
+            jr = rows[j0:j1]
+            h = eh[jr]
             x = h[:, None, :] * t[None, :, :]                          # model.py:70
             if dist:                                                   # model.py:265-267
-                ll = torch.abs(cf[c0:c1][None, :, :] - cf[j0:j1][:, None, :]).to(torch.float32)
+                ll = torch.abs(cf[c0:c1][None, :, :] - cf[jr][:, None, :]).to(torch.float32)
                 x = torch.cat([x, torch.sigmoid(torch.nn.functional.linear(ll * 100, wd, bd))], -1)
                 del ll
             r1 = torch.relu(torch.nn.functional.linear(x, w1, b1))     # model.py:71
             e = torch.exp(torch.nn.functional.linear(r1, w2)).squeeze(-1)   # model.py:73-76
-            lo, hi = max(j0, c0), min(j1, c1)
-            if lo < hi:                                                # model.py:77-78: j == c
-                d = torch.arange(lo, hi, device=device)
-                e[d - j0, d - c0] = 0.0
+            self_ = (jr >= c0) & (jr < c1)                             # model.py:77-78: j == c
+            if bool(self_.any()):
+                q = torch.nonzero(self_).squeeze(1)
+                e[q, jr[q] - c0] = 0.0
             E[j0:j1] = e
             ES[j0:j1] = e * (h @ t.T)
         S = A @ E                                                      # [U, w]

@@ -357,3 +357,45 @@ def test_config4_region_distance_job_every_user_full_catalog():
     print(f"config 4 region_distance, all {U} users x all {P} POIs vs the torch pairs checker: max "
           f"|winner score diff| {dw:.3g}; {same} users' top-50 equal the checker's as sets; largest "
           f"excess of a non-winner over the weakest winner {over:.3g} (allowed: {TIE_ULPS} ulps)")
+
+
+def test_config2_job_every_user_full_catalog():
+    """Config 2 (bench.py --config 2: 10,000 users x 50,000 POIs, d = H = 64, h <= 100, the bench's
+    seeds) through the pairs route with the bench's knobs: every user against every candidate
+    with the torch pairs checker (tests/_torch_pairs.py), as the config-4 test above."""
+    from _torch_pairs import check_against_full_catalog, full_catalog_topk
+    from poi_recommendation_models_amd.catalog import DeviceCSR, _score_topk_pairs
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    U, P, D, H, K = 10_000, 50_000, 64, 64, 50
+    data = make_checkins(U, P, 100, seed=2024)
+    p = init_nais_params(P, D, H, seed=7, emb_std=0.3, bias_std=0.1)
+    m = _model(p, P, D, H)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    ids, sc = _score_topk_pairs(m, csr, np.arange(U), K, None, None, None, None, force=True)
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    ti, tv, at = full_catalog_topk(p, data.indptr, data.indices, P, 60, ids, DEV)
+    dw, same, over = check_against_full_catalog(ids, sc, ti, tv, at, SCORE_ATOL, TIE_ULPS)
+    print(f"config 2, all {U} users x all {P} POIs vs the torch pairs checker: max |winner score diff| "
+          f"{dw:.3g}; {same} users' top-50 equal the checker's as sets; largest excess {over:.3g}")
+
+
+def test_config5_direct_64_users_full_catalog():
+    """Config 5 (200,000 users x 1,000,000 POIs, d = H = 128, h <= 200; bench.py --config 5 times
+    the direct route on the first users): the first 64 users through the direct route, each
+    against all 10^6 candidates with the torch pairs checker (its rows: the 64 users' distinct
+    history POIs only)."""
+    from _torch_pairs import check_against_full_catalog, full_catalog_topk
+    from poi_recommendation_models_amd.catalog import DeviceCSR, score_topk
+    from poi_recommendation_models_amd.synthetic import init_nais_params, make_checkins
+    U, P, D, H, K, NU = 200_000, 1_000_000, 128, 128, 50, 64
+    data = make_checkins(U, P, 200, seed=2024)
+    p = init_nais_params(P, D, H, seed=7, emb_std=0.3, bias_std=0.1)
+    m = _model(p, P, D, H)
+    csr = DeviceCSR.from_arrays(data.indptr, data.indices, P, DEV)
+    ids, sc = score_topk(m, csr, np.arange(NU), K, strategy="direct")
+    ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
+    ip = data.indptr[:NU + 1]
+    ti, tv, at = full_catalog_topk(p, ip, data.indices[:ip[-1]], P, 60, ids, DEV, jchunk=4096)
+    dw, same, over = check_against_full_catalog(ids, sc, ti, tv, at, SCORE_ATOL, TIE_ULPS)
+    print(f"config 5, {NU} users x all {P} POIs (direct route) vs the torch pairs checker: max |winner "
+          f"score diff| {dw:.3g}; {same} users' top-50 equal the checker's as sets; largest excess {over:.3g}")
