@@ -279,8 +279,22 @@ PAIR_BOUNDED_STRIPE = 512       # columns per bounded-gather wave (nais_pairs.hi
 _masked: dict = {}
 
 
+def bounded_gather_cu_seconds(entries, NC, users, k):
+    """CU-seconds of one job's bounded gathers (nais_pair_bound_topk, one launch per 512-column
+    stripe), fitted on the measured launches (profiles/r6/split_world, profiles/r6/configs):
+      entries x NC x 4 B / 90.4 GB/s   the hi words streamed (Infinity-Cache served)
+      + 722 ns x users x launches      per user and launch: its lists in and out, its CSR rows
+      + 68 ns x insertions             a user's running top-k takes ~k (1 + ln(NC / k)) of them
+    Config 4 at N = 1 / 2 / 4 / 8 column shards (68 gather CUs: 157.9 / 165.9 / 176.9 / 194.9
+    CU-ms per launch) and config 2 (24 CUs: 21.4 CU-ms per launch for 10,000 users with h <= 100)
+    within 1-3 %: narrow shards and short histories pay the per-user terms on fewer bytes."""
+    launches = np.ceil(NC / PAIR_BOUNDED_STRIPE)
+    ins = k * (1.0 + np.log(max(float(NC), float(k)) / k))
+    return entries * NC * 4.0 / 90.4e9 + 722e-9 * users * launches + 68e-9 * users * ins
+
+
 def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, work_queues=True,
-                   gather_bytes=8):
+                   gather_bytes=8, k=None, users=None):
     """CUs for the table stream (the rest gather), in steps of ncu / 8 (counts off a multiple of 32
     leave a shader engine short and lose -- DESIGN.md, CU split), from a cost model fitted
     on config 4 and config 5 (profiles/r1/cfg5p/, re-fitted in round 3 on the fp16x6 tables:
@@ -311,7 +325,10 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     x6n = (PAIR_WORK_QUEUE and work_queues and products == 6 and D in (32, 64, 128) and H <= 128
            and not prior)
     step = min(PAIR_SPLIT_STEP, xcd) if x6n else xcd
-    rate = 1.5e15 if x6n else 1.25e15   # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard)
+    # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard); round 6 keeps config 4's figure: the
+    # bounded route's N = 1 / 2 shards measured 188 / 188 best (profiles/r6/split_world), which 1.5e15
+    # put at 188 / 184
+    rate = 1.45e15 if x6n else 1.25e15
     din_k = D + (2 if dist else 0)      # the width the kernels multiply (padded)
     t_tab = J * NC * 2.0 * H * din_k * products / (1.3e14 if products == 1 else rate)
     if x6n and dist:
@@ -330,12 +347,13 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
         # profiles/r6/bounded, split_ab), and 4-CU steps: 188 / 68 ran 471.4 ms against 476.9 /
         # 480.2 at 184 / 72 and 490.8 at 180 / 76 on one box (profiles/r6/split_ab)
         per_cu = 66e9
-        if block_bytes is not None and block_bytes / 2 <= 128e6:
-            # a hi stripe of half the Infinity Cache or less (config 2: 102 MB) is served faster:
-            # 95 GB/s per CU measured at 24 gather CUs (87.5 ms for 0.2 TB, profiles/r6/split_ab)
-            per_cu = 95e9
         if x6n:
             step = 4
+        if users and k:
+            # the three-term fit (bounded_gather_cu_seconds) as an effective per-CU rate: one
+            # rank's narrow column shard (N = 8: best split 172-180 against 188 at N = 1,
+            # profiles/r6/split_world) and short histories (config 2) pay more per byte
+            per_cu = gbytes / bounded_gather_cu_seconds(entries, NC, users, k)
     cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
@@ -604,7 +622,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
             # the fused gather (the score-row gather and nais_dot_pair_table keep fixed grids)
             wq_both = fused and type(model)._pair_table is _NAISDevice._pair_table
             table_cus = (auto_table_cus(model, J, NC, entries, ncu, prior is not None, J * ld * 8,
-                                        work_queues=wq_both, gather_bytes=4 if bnd[0] else 8)
+                                        work_queues=wq_both, gather_bytes=4 if bnd[0] else 8, k=k,
+                                        users=m)
                          if PAIR_TABLE_CUS < 0 else PAIR_TABLE_CUS)
             wq_on[0] = table_cus % max(1, ncu // 8) != 0
             if events is not None:

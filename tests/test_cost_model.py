@@ -2,6 +2,8 @@
 measured A/Bs picked (CU split) and the shader-engine granularity."""
 import types
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -81,3 +83,32 @@ def test_bench_kernel_label_mirrors_dispatch(precision, D, H, mode, want):
     name = bench.table_kernel_name(precision, D, H, mode=mode)
     want = want if want.startswith("catalog") else f"catalog_score_{want}_kernel"
     assert name.split(" ")[0] == want
+
+
+@pytest.mark.parametrize("world,want", [(1, 188), (2, 188), (4, 184), (8, 176)])
+def test_bounded_route_splits_by_shard_width(world, want):
+    """The bounded gather's three-term cost (catalog.bounded_gather_cu_seconds): one rank's column
+    shard of config 4 (all 50,000 users, P / N columns) pays the per-user and insertion terms on
+    fewer bytes, so narrow shards give the gather more CUs (measured best: 188 / 188 / 180 /
+    172-180 at N = 1 / 2 / 4 / 8, profiles/r6/split_world)."""
+    NC = (100_000 + world - 1) // world
+    n = auto_table_cus(_model(64, 64, "fp16x6"), 100_000, NC, 5_030_351, 256, False,
+                       100_000 * 512 * 8, gather_bytes=4, k=50, users=50_000)
+    assert n == want
+
+
+def test_bounded_route_config2_split():
+    """Config 2 (10,000 users, h <= 100, 50,000 POIs): 232 / 24, its measured split (96.2 ms,
+    profiles/r6/configs); the per-user term prices its short histories (48 GB/s per gather CU)."""
+    assert auto_table_cus(_model(64, 64, "fp16x6"), 49_999, 50_000, 505_318, 256, False,
+                          49_999 * 512 * 8, gather_bytes=4, k=50, users=10_000) == 232
+
+
+def test_bounded_gather_cost_fit():
+    """The fit reproduces the measured launches it was fitted on within 3 %."""
+    from poi_recommendation_models_amd.catalog import bounded_gather_cu_seconds
+    for NC, cu_ms in ((100_000, 157.9), (50_000, 165.9), (25_000, 176.9), (12_500, 194.9)):
+        per_launch = bounded_gather_cu_seconds(5_030_351, NC, 50_000, 50) / np.ceil(NC / 512)
+        assert abs(per_launch * 1e3 / cu_ms - 1) < 0.03, (NC, per_launch)
+    per_launch = bounded_gather_cu_seconds(505_318, 50_000, 10_000, 50) / 98
+    assert abs(per_launch * 1e3 / 21.42 - 1) < 0.03
