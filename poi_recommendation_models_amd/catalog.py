@@ -237,6 +237,9 @@ PAIR_BLOCK_COLS = 512
 # every CU).
 PAIR_TABLE_CUS = -1
 PAIR_FIRST_TABLE_ALL_CUS = True   # block 0's table (nothing to overlap it with) on every CU
+# (The mirror image -- the last block's gather on every CU behind its table -- was neutral: config 4
+# 475.3 / 476.9 vs 475.5 / 475.7 ms, one rank of N = 8 76.0 / 76.7 vs 76.0 / 75.6 ms, interleaved on
+# one box, profiles/r6/last_gather_ab; not kept.)
 # Fused gather + running top-k (nais_pair_gather_topk): each user keeps its best k keys while the
 # stripes stream by, so no [users, P] score rows are formed and no top-k pass reads them back
 # (k <= 256, models without a post-gather score fixup).
