@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define NAIS_ABI_VERSION 13   /* 13: split16 pair tables, bounded gather + exact refine (nais_pair_table_split, nais_pair_bound_topk, nais_pair_refine_topk); 12: any embed_dim <= 256 and any hidden (generic-shape kernels); 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
+#define NAIS_ABI_VERSION 14   /* 14: nais_pair_bound_topk / nais_pair_refine_topk take the optional per-entry table rows and per-slot history spans; 13: split16 pair tables, bounded gather + exact refine (nais_pair_table_split, nais_pair_bound_topk, nais_pair_refine_topk); 12: any embed_dim <= 256 and any hidden (generic-shape kernels); 11: hidden up to 256 (fp16x6 scoring, nais_forward), any variant on the x6n kernel */
 
 /* model variants */
 #define NAIS_VARIANT_BASIC 0           /* NAIS_basic                      model.py:8-97    */
@@ -291,6 +291,12 @@ int32_t nais_topk_keys_finish(const uint64_t* keys, const int32_t* kcount, int32
  *                      that can reach the global top-k: kcount may be < k (padding as short lists).
  *                      A column shard's k-th lower key is a lower bound of the global k-th exact key,
  *                      so every global winner on this shard is still returned.
+ *   entry_rows (both; may be NULL): entry_rows[e] = rowmap[indices[e]] for every CSR entry e of the
+ *                      listed users -- the table row of each history entry, read beside its POI id
+ *                      instead of after it. spans (nais_pair_bound_topk; may be NULL):
+ *                      spans[2*s] = indptr[users[s]], spans[2*s+1] = the history length of users[s]
+ *                      -- one load per slot instead of two in a row. Both only shorten the chains
+ *                      of dependent loads (ABI 14); the results are the same with or without them.
  */
 int32_t nais_pair_table_split(const nais_params_t* params, const int64_t* items, int64_t num_items,
                               int64_t col0, int64_t cols, const int64_t* region_of,
@@ -300,7 +306,8 @@ int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowm
                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
                              uint64_t* lo_keys, int32_t* lo_count, uint64_t* surv, int32_t* surv_count,
-                             int32_t surv_cap, int32_t* work, void* stream);
+                             int32_t surv_cap, const int32_t* entry_rows, const int64_t* spans,
+                             int32_t* work, void* stream);
 int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                               int64_t ld, int64_t block_cols, const int32_t* rowmap,
                               const int64_t* indptr, const int64_t* indices, const int32_t* users,
@@ -308,7 +315,7 @@ int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                               const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
                               const int32_t* surv_count, int32_t surv_cap, const uint64_t* tau,
                               uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* stats,
-                              void* stream);
+                              const int32_t* entry_rows, void* stream);
 /*
  * Power-law prior on the pairs route (powerLaw.py:86-92, run.py:537-539; the direct route's
  * nais_score_topk with a prior computes the same G rows per user):

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libnais_hip.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 PRECISION_FP32, PRECISION_FP16X3, PRECISION_FP16X3_PAIRSPLIT = 0, 1, 2
 PRIOR_FINITE = 1   # nais_pair_prior_gather flags (include/nais.h NAIS_PRIOR_FINITE)
 PRECISION_FP16X6, PRECISION_FP16X6_PAIRSPLIT = 3, 4
@@ -229,10 +229,10 @@ def load(path: str | None = None):
                                           vp, i64, vp, vp]
     lib.nais_pair_bound_topk.restype = i32
     lib.nais_pair_bound_topk.argtypes = [vp, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32, vp, vp, vp, vp,
-                                         i32, vp, vp]
+                                         i32, vp, vp, vp, vp]
     lib.nais_pair_refine_topk.restype = i32
     lib.nais_pair_refine_topk.argtypes = [vp, i64, i64, i64, vp, vp, vp, vp, i32, i64, i64, f32, i32,
-                                          vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]
+                                          vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp, vp]
     lib.nais_stream_create_cu_mask.restype = i32
     lib.nais_stream_create_cu_mask.argtypes = [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]
     lib.nais_stream_destroy.restype = i32

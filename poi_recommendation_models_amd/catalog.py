@@ -278,6 +278,9 @@ PAIR_SPLIT_STEP = 8
 # the memory budget; otherwise the exact fused gather runs on double-buffered tables.
 PAIR_BOUNDED = True
 PAIR_SURV_CAP = 1024            # survivor keys per user (compacted by the current bound when full)
+# the bounded gather / refine get each CSR entry's table row and each slot's history span (ABI 14:
+# shorter chains of dependent loads); "0" passes NULL (A/B only)
+PAIR_SHORT_CHAINS = os.environ.get("NAIS_PAIR_SHORT_CHAINS", "1") != "0"
 PAIR_BOUNDED_STRIPE = 512       # columns per bounded-gather wave (nais_pairs.hip BSTRIPE)
 _masked: dict = {}
 
@@ -286,14 +289,18 @@ def bounded_gather_cu_seconds(entries, NC, users, k):
     """CU-seconds of one job's bounded gathers (nais_pair_bound_topk, one launch per 512-column
     stripe), fitted on the measured launches (profiles/r6/split_world, profiles/r6/configs):
       entries x NC x 4 B / 90.4 GB/s   the hi words streamed (Infinity-Cache served)
-      + 722 ns x users x launches      per user and launch: its lists in and out, its CSR rows
+      + 512 ns x users x launches      per user and launch: its lists in and out, its CSR rows
       + 68 ns x insertions             a user's running top-k takes ~k (1 + ln(NC / k)) of them
-    Config 4 at N = 1 / 2 / 4 / 8 column shards (68 gather CUs: 157.9 / 165.9 / 176.9 / 194.9
-    CU-ms per launch) and config 2 (24 CUs: 21.4 CU-ms per launch for 10,000 users with h <= 100)
-    within 1-3 %: narrow shards and short histories pay the per-user terms on fewer bytes."""
+    Fitted first (722 ns per user and launch) on config 4 at N = 1 / 2 / 4 / 8 column shards (68
+    gather CUs: 157.9 / 165.9 / 176.9 / 194.9 CU-ms per launch) and on config 2 (24 CUs: 21.4 CU-ms
+    per launch for 10,000 users with h <= 100), within 1-3 %. Narrow shards and short histories pay
+    the per-user terms on fewer bytes. The per-user term is latency: a chain of dependent loads at
+    a few waves per SIMD. The per-entry rows, the per-slot spans and 4 rows in flight (4 waves per
+    SIMD) brought it to 512 ns: config 4 2.168 ms x 68 CUs, N = 8 2.28 ms x 80 CUs per launch
+    (profiles/r6/chains_ab)."""
     launches = np.ceil(NC / PAIR_BOUNDED_STRIPE)
     ins = k * (1.0 + np.log(max(float(NC), float(k)) / k))
-    return entries * NC * 4.0 / 90.4e9 + 722e-9 * users * launches + 68e-9 * users * ins
+    return entries * NC * 4.0 / 90.4e9 + 512e-9 * users * launches + 68e-9 * users * ins
 
 
 def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, work_queues=True,
@@ -360,6 +367,11 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
+        if gather_bytes == 4 and step < xcd and (ncu - n) % xcd == 0:
+            # a bounded gather on exactly whole XCDs (contiguous CU ids: 64 = two of them) ran
+            # both streams slower than the split 4 CUs over it (config 4: 192 / 64 497 ms against
+            # 484 at 188 / 68, three interleaved pairs on one box, profiles/r6/split_n1)
+            continue
         t = max(t_tab * ncu / n, gbytes / min(cap, (ncu - n) * per_cu))
         if best_t is None or t <= best_t:   # ties (gather-bound): the larger table share
             best, best_t = n, t
@@ -573,7 +585,9 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                         u_dev.data_ptr() + 4 * a, b - a, c0, w, float(model.beta), k,
                         lokeys.data_ptr() + 8 * k * a, locount.data_ptr() + 4 * a,
                         surv.data_ptr() + 8 * PAIR_SURV_CAP * a, scount.data_ptr() + 4 * a, PAIR_SURV_CAP,
-                        wq(stream_), stream_), "nais_pair_bound_topk")
+                        _capi.ptr(erows), spans.data_ptr() + 16 * a if spans is not None else None,
+                        wq(stream_), stream_),
+                        "nais_pair_bound_topk")
                     return
                 _capi.check(lib.nais_pair_gather_topk(
                     tab[0].data_ptr(), tab[1].data_ptr(), ld, rowmap.data_ptr(), csr.indptr.data_ptr(),
@@ -618,6 +632,14 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 locount = torch.zeros(m, dtype=torch.int32, device=dev)
                 surv = torch.empty(m, PAIR_SURV_CAP, dtype=torch.int64, device=dev)
                 scount = torch.zeros(m, dtype=torch.int32, device=dev)
+                # the gathers' load chains shortened (include/nais.h, ABI 14): each CSR entry's
+                # table row, and each slot's (history start, length)
+                erows = spans = None
+                if PAIR_SHORT_CHAINS:
+                    erows = rowmap.index_select(0, csr.indices)
+                    hb_ = csr.indptr.index_select(0, u_dev.to(torch.int64))
+                    spans = torch.stack([hb_, csr.indptr.index_select(0, u_dev.to(torch.int64) + 1) - hb_],
+                                        1).contiguous()
                 if events is not None:
                     events.append(("bounded", None, None, 1))
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -699,7 +721,8 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                 for t_ in tss:
                     torch_stream.wait_stream(t_)
                 for t in [*tabs, *pr_of.values(), *([wq_slots] if wq_slots is not None else []),
-                          *((*arena, lokeys, locount, surv, scount) if bnd[0] else ())]:
+                          *((*arena, lokeys, locount, surv, scount,
+                             *((erows, spans) if erows is not None else ())) if bnd[0] else ())]:
                     for t_ in (*tss, gs):   # not handed to the main stream early
                         t.record_stream(t_)
             if bnd[0]:   # the exact refine of every user's surviving candidates (all CUs)
@@ -713,10 +736,10 @@ def _score_topk_pairs(model, train_matrix, users, k, region_of, coords, latlon_m
                     csr.indices.data_ptr(), u_dev.data_ptr(), m, c0_all, NC, float(model.beta), k,
                     lokeys.data_ptr(), locount.data_ptr(), surv.data_ptr(), scount.data_ptr(),
                     PAIR_SURV_CAP, tau_g.data_ptr() if tau_g is not None else None, keys.data_ptr(),
-                    kcount.data_ptr(), counters[0:1].data_ptr(), stats.data_ptr(), st),
+                    kcount.data_ptr(), counters[0:1].data_ptr(), stats.data_ptr(), _capi.ptr(erows), st),
                     "nais_pair_refine_topk"))
                 model._last_bound_stats = stats
-                del arena, lokeys, locount, surv, scount
+                del arena, lokeys, locount, surv, scount, erows, spans
             del tabs
             pr_of.clear()
             if not fused:

@@ -538,6 +538,14 @@ prior_pair_gather_kernel(const double* __restrict__ pr, int64_t ld, const int32_
 // same fp32 bits, read as one (e, e*s) pair per row from the ex table -- and ranks them: the same
 // top-k lists, ids and score bits, as the exact gather.
 // Keys as pair_gather_topk_kernel: ordered(score) << 32 | (0xFFFFFFFF - poi).
+// Rows in flight per bounded-gather wave. 4: 116 VGPRs, 4 waves per SIMD; 8 held 148 VGPRs, 3 waves.
+// Its chain of dependent loads per user (span, ids and rows, list state) hides better with more
+// waves. Per launch 2.224 -> 2.168 ms at config 4 and 2.45 -> 2.28 ms on one rank of N = 8, in
+// interleaved runs (profiles/r6/chains_ab). Performance only: A/B builds may set it.
+#ifndef NAIS_PAIRS_BGU
+#define NAIS_PAIRS_BGU 4
+#endif
+constexpr int BGU = NAIS_PAIRS_BGU;
 constexpr int BCPL = 8;                       // columns per lane: 32-byte hi rows per lane
 constexpr int BSTRIPE = 64 * BCPL;            // 512 columns per wave (one launch per block)
 constexpr int BK_LDS = 512;                   // keys per wave in LDS: k + 256 offered (k <= 256)
@@ -576,12 +584,12 @@ __device__ __forceinline__ void bound_rows(const uint32_t* __restrict__ HI, int6
     v[1] = uint4{b[0], b[1], b[2], b[3]};
   };
   int jj = 0;
-  for (; jj + GU <= jn; jj += GU) {
-    uint4 v[GU][2];
+  for (; jj + BGU <= jn; jj += BGU) {
+    uint4 v[BGU][2];
 #pragma unroll
-    for (int g = 0; g < GU; ++g) ld2(row(jj + g), v[g]);
+    for (int g = 0; g < BGU; ++g) ld2(row(jj + g), v[g]);
 #pragma unroll
-    for (int g = 0; g < GU; ++g) acc(v[g]);
+    for (int g = 0; g < BGU; ++g) acc(v[g]);
   }
   for (; jj < jn; ++jj) {
     uint4 v[2];
@@ -719,7 +727,8 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
                        const int32_t* __restrict__ users, int32_t nusers, int64_t col0, int64_t cols,
                        float beta, int k, unsigned long long* __restrict__ lokeys,
                        int32_t* __restrict__ locount, unsigned long long* __restrict__ surv,
-                       int32_t* __restrict__ scount, int cap, int32_t* __restrict__ work) {
+                       int32_t* __restrict__ scount, int cap, const int32_t* __restrict__ erows,
+                       const int64_t* __restrict__ spans, int32_t* __restrict__ work) {
   __shared__ unsigned long long lk[GW][BK_LDS];
   __shared__ uint32_t hm[GW][BSTRIPE / 32];   // history POIs of this block, one bit per column
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -740,8 +749,21 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
     slot = int64_t(blockIdx.x) * GW + w;
   }
   if (slot >= nusers) break;                 // wave-uniform; no workgroup barriers below
-  const int64_t u = users[slot];
-  const int64_t hb = indptr[u], hl = indptr[u + 1] - hb;
+  // the slot's history span: one load with spans (else users[slot] -> indptr, two in a row)
+  int64_t hb, hl;
+  if (spans) {
+    hb = spans[2 * slot];
+    hl = spans[2 * slot + 1];
+  } else {
+    const int64_t u = users[slot];
+    hb = indptr[u];
+    hl = indptr[u + 1] - hb;
+  }
+  // the slot's list state, loaded before the gather (independent of it): its latency overlaps
+  // the row reads instead of following them
+  const int cnt = locount[slot];
+  const unsigned long long lk_last = lokeys[slot * k + k - 1];   // meaningful when cnt == k
+  int sc = scount[slot];
   const int64_t x = int64_t(lane) * BCPL;    // column within the block [col0, col0 + cols)
   if (lane < BSTRIPE / 32) hm[w][lane] = 0u;
   wave_lds_sync();
@@ -755,8 +777,10 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
     const int jn = __builtin_amdgcn_readfirstlane((int)std::min<int64_t>(64, hl - j0));
     int32_t mrow = 0;
     if (lane < jn) {
-      const int64_t c = indices[hb + j0 + lane];
-      mrow = rowmap[c];
+      // with erows the entry's table row loads beside its POI id (else rowmap[id], after it)
+      const int64_t e = hb + j0 + lane;
+      const int64_t c = indices[e];
+      mrow = erows ? erows[e] : rowmap[c];
       const int64_t r = c - col0;
       if (r >= 0 && r < cols) atomicOr(&hm[w][r >> 5], 1u << (r & 31));
     }
@@ -769,8 +793,7 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
     S[q] = S2[q / 2][q & 1];
     N[q] = N2[q / 2][q & 1];
   }
-  const int cnt = locount[slot];
-  const unsigned long long thr = cnt == k ? lokeys[slot * k + k - 1] : 0ull;   // valid keys are > 0
+  const unsigned long long thr = cnt == k ? lk_last : 0ull;   // valid keys are > 0
   // upper keys of every candidate; lower keys only where the upper one reaches thr (else neither
   // can enter the list nor survive). Held as their score halves (the id half is the column's), so
   // the epilogue does not outgrow the gather loop's registers.
@@ -828,7 +851,6 @@ pair_bound_topk_kernel(const uint32_t* __restrict__ HI, int64_t ld, const int32_
   }
   const int m = __shfl(excl, 63);
   excl -= mine_n;
-  int sc = scount[slot];
   if (m > 0 && sc >= 0) {
     unsigned long long* list = surv + slot * (int64_t)cap;
     if (sc + m > cap) {   // compact by the current tau (in place: a write never passes the chunk read)
@@ -875,7 +897,7 @@ pair_refine_topk_kernel(const uint2* __restrict__ X, int64_t bstride, int64_t ld
                         const int32_t* __restrict__ scount, int cap,
                         const unsigned long long* __restrict__ tau_in, unsigned long long* __restrict__ keys,
                         int32_t* __restrict__ kcount, int32_t* __restrict__ nan_count,
-                        int32_t* __restrict__ stats) {
+                        int32_t* __restrict__ stats, const int32_t* __restrict__ erows) {
   __shared__ unsigned long long lk[GW][RF_LDS];
   __shared__ uint32_t cb[GW][128];   // pending candidate columns (relative to col0)
   __shared__ unsigned long long ck[GW][RF_CAND];   // kept survivors' upper keys, sorted
@@ -906,7 +928,7 @@ pair_refine_topk_kernel(const uint2* __restrict__ X, int64_t bstride, int64_t ld
       int64_t mine = 0, mid = -1;
       if (lane < jn) {
         mid = indices[hb + j0 + lane];
-        mine = int64_t(rowmap[mid]) * ld;   // ex rows hold ld pairs
+        mine = int64_t(erows ? erows[hb + j0 + lane] : rowmap[mid]) * ld;   // ex rows hold ld pairs
       }
       const uint32_t mlo = uint32_t(mine), mhi = uint32_t(mine >> 32);
       const uint32_t ilo = uint32_t(mid), ihi = uint32_t(mid >> 32);
@@ -1132,7 +1154,8 @@ int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowm
                              const int64_t* indptr, const int64_t* indices, const int32_t* users,
                              int32_t num_users, int64_t col0, int64_t cols, float beta, int32_t k,
                              uint64_t* lo_keys, int32_t* lo_count, uint64_t* surv, int32_t* surv_count,
-                             int32_t surv_cap, int32_t* work, void* stream) {
+                             int32_t surv_cap, const int32_t* entry_rows, const int64_t* spans,
+                             int32_t* work, void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || ld < cols || k <= 0 || surv_cap < 64)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
   if (k > BK_LDS - 256) return nais_internal_fail(NAIS_E_UNSUPPORTED, "k must be <= 256");
@@ -1155,7 +1178,8 @@ int32_t nais_pair_bound_topk(const uint32_t* hi, int64_t ld, const int32_t* rowm
     hipLaunchKernelGGL(pair_bound_topk_kernel, dim3(groups), dim3(GW * 64), 0, st, hi + s0, ld, rowmap,
                        indptr, indices, users, num_users, col0 + s0, std::min<int64_t>(BSTRIPE, cols - s0),
                        beta, (int)k, reinterpret_cast<unsigned long long*>(lo_keys), lo_count,
-                       reinterpret_cast<unsigned long long*>(surv), surv_count, (int)surv_cap, work);
+                       reinterpret_cast<unsigned long long*>(surv), surv_count, (int)surv_cap, entry_rows,
+                       spans, work);
     const int32_t rc = nais_internal_check_launch("pair_bound_topk_kernel");
     if (rc) return rc;
   }
@@ -1169,7 +1193,7 @@ int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                               const uint64_t* lo_keys, const int32_t* lo_count, const uint64_t* surv,
                               const int32_t* surv_count, int32_t surv_cap, const uint64_t* tau,
                               uint64_t* keys, int32_t* kcount, int32_t* nan_count, int32_t* stats,
-                              void* stream) {
+                              const int32_t* entry_rows, void* stream) {
   if (num_users < 0 || col0 < 0 || cols < 0 || k <= 0 || surv_cap < 64 || block_cols <= 0 ||
       ld < std::min<int64_t>(block_cols, cols) || block_stride < 0 || block_stride % 2 != 0)
     return nais_internal_fail(NAIS_E_INVALID, "bad shape");
@@ -1186,7 +1210,7 @@ int32_t nais_pair_refine_topk(const uint32_t* ex, int64_t block_stride,
                      reinterpret_cast<const unsigned long long*>(lo_keys), lo_count,
                      reinterpret_cast<const unsigned long long*>(surv), surv_count, (int)surv_cap,
                      reinterpret_cast<const unsigned long long*>(tau),
-                     reinterpret_cast<unsigned long long*>(keys), kcount, nan_count, stats);
+                     reinterpret_cast<unsigned long long*>(keys), kcount, nan_count, stats, entry_rows);
   return nais_internal_check_launch("pair_refine_topk_kernel");
 }
 
