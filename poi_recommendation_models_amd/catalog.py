@@ -358,7 +358,11 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
         # 480.2 at 184 / 72 and 490.8 at 180 / 76 on one box (profiles/r6/split_ab)
         per_cu = 66e9
         if x6n:
-            step = 4
+            # 2-CU steps: config 4 at 190 / 66 ran 476.2 / 476.8 / 478.6 ms against 482.4-482.5 at
+            # 188 / 68, interleaved on one box (profiles/r6/split_n1); one rank of N = 2 at 190
+            # 239.0 / 239.3 vs 240.5 / 240.9 at 188, N = 4 at 186 even with 184, config 2 at 234
+            # 95.8 / 96.2 vs 95.5 / 95.9 at 232 (profiles/r6/split_n1/step2)
+            step = 2
         if users and k:
             # the three-term fit (bounded_gather_cu_seconds) as an effective per-CU rate: one
             # rank's narrow column shard (N = 8: best split 172-180 against 188 at N = 1,
