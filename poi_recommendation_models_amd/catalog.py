@@ -279,7 +279,8 @@ PAIR_SPLIT_STEP = 8
 PAIR_BOUNDED = True
 PAIR_SURV_CAP = 1024            # survivor keys per user (compacted by the current bound when full)
 # the bounded gather / refine get each CSR entry's table row and each slot's history span (ABI 14:
-# shorter chains of dependent loads); "0" passes NULL (A/B only)
+# shorter chains of dependent loads); "0" passes NULL (A/B only). Per gather launch 2.272 -> 2.224
+# ms at config 4, 2.48 -> 2.45 ms on one rank of N = 8, interleaved (profiles/r6/chains_ab)
 PAIR_SHORT_CHAINS = os.environ.get("NAIS_PAIR_SHORT_CHAINS", "1") != "0"
 PAIR_BOUNDED_STRIPE = 512       # columns per bounded-gather wave (nais_pairs.hip BSTRIPE)
 _masked: dict = {}
