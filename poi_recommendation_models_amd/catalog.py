@@ -372,12 +372,15 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     cap = 7.5e12   # the memory side's rate for the gather, chip-wide
     best, best_t = ncu // 2, None
     for n in range((ncu // 4 + step - 1) // step * step, ncu - step + 1, step):
-        if gather_bytes == 4 and step < xcd and (ncu - n) % xcd == 0:
-            # a bounded gather on exactly whole XCDs (contiguous CU ids: 64 = two of them) ran
-            # both streams slower than the split 4 CUs over it (config 4: 192 / 64 497 ms against
-            # 484 at 188 / 68, three interleaved pairs on one box, profiles/r6/split_n1)
-            continue
-        t = max(t_tab * ncu / n, gbytes / min(cap, (ncu - n) * per_cu))
+        g_pen = 1.0
+        if gather_bytes == 4 and PAIR_CU_LAYOUT == "contiguous" and (ncu - 1) // xcd - n // xcd + 1 <= 2:
+            # a bounded gather confined to two XCDs (contiguous CU ids) costs ~4 % more CU-time per
+            # launch than one spanning three: config 4 at 192 / 64 151.5 CU-ms against 146.2 at
+            # 190 / 66 (the job 497 vs 484 ms, profiles/r6/split_n1), region_distance at 196 / 60
+            # 151.9 -- whose job ran 522.6 / 524.4 ms there against 514.2 / 516.6 at 194 / 62
+            # (profiles/r6/rd_split)
+            g_pen = 1.04
+        t = max(t_tab * ncu / n, gbytes * g_pen / min(cap, (ncu - n) * per_cu))
         if best_t is None or t <= best_t:   # ties (gather-bound): the larger table share
             best, best_t = n, t
     return best
