@@ -336,10 +336,11 @@ def auto_table_cus(model, J, NC, entries, ncu, prior=False, block_bytes=None, wo
     x6n = (PAIR_WORK_QUEUE and work_queues and products == 6 and D in (32, 64, 128) and H <= 128
            and not prior)
     step = min(PAIR_SPLIT_STEP, xcd) if x6n else xcd
-    # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard); round 6 keeps config 4's figure: the
-    # bounded route's N = 1 / 2 shards measured 188 / 188 best (profiles/r6/split_world), which 1.5e15
-    # put at 188 / 184
-    rate = 1.45e15 if x6n else 1.25e15
+    # round 4: 1.45e15 (config 4), 1.55e15 (config-5 shard); round 6: 1.47e15 -- the final tree's
+    # config-4 tables ran 446.5 ms on 190 CUs (1.45e15 said 456.8), and 1.47e15 keeps every
+    # measured best split: 190 / 190 / 186 / 180 at N = 1 / 2 / 4 / 8 (profiles/r6/split_n1,
+    # split_world) and region_distance at 194 (profiles/r6/rd_split), where 1.45e15 chose 196
+    rate = 1.47e15 if x6n else 1.25e15
     din_k = D + (2 if dist else 0)      # the width the kernels multiply (padded)
     t_tab = J * NC * 2.0 * H * din_k * products / (1.3e14 if products == 1 else rate)
     if x6n and dist:

@@ -113,3 +113,12 @@ def test_bounded_gather_cost_fit():
     for NC, cu_ms in ((100_000, 2.168 * 68), (12_500, 2.28 * 80)):
         per_launch = bounded_gather_cu_seconds(5_030_351, NC, 50_000, 50) / np.ceil(NC / 512)
         assert abs(per_launch * 1e3 / cu_ms - 1) < 0.03, (NC, per_launch)
+
+
+def test_region_distance_bounded_split():
+    """bench.py's region_distance leg on the bounded route: 194 / 62 (measured 514.2 / 516.6 ms
+    against 522.6 / 524.4 at 196 / 60 and 530 at 190 / 66, profiles/r6/rd_split)."""
+    m = _model(66, 64, "fp16x6")
+    m.VARIANT = 2            # NAIS_VARIANT_REGION_DISTANCE
+    assert auto_table_cus(m, 100_000, 100_000, 5_030_351, 256, False, 100_000 * 512 * 8,
+                          gather_bytes=4, k=50, users=50_000) == 194
